@@ -1,0 +1,288 @@
+"""Generate the golden fixtures under tests/golden/ from the reference itself.
+
+Run in the build container only (needs /root/reference):
+
+    python tests/golden/make_golden.py
+
+Every fixture is DATA: inputs + the reference's outputs on them.  The
+reference is imported with in-memory numba/netCDF4 stubs (``refharness.py``);
+its own functions produce every expected value below:
+
+* ``bg_<kind>.npz``     sha256 + samples of ``BS.fields`` after ``BS.ready``   (bs.py:318-372)
+* ``merc_<kind>.npz``   ``cal_bs_mercator_point(mode='numpy')`` on 2 048 points (bs.py:781-887)
+* ``rhs_<kind>.npz``    ``WR.diffun_numpy`` on 4 096 states incl. edge cases   (wr.py:492-556)
+* ``step_<kind>.npz``   ``rk_step`` + error norm on 1 024 (y, f, h)             (rkf45.py:259-373)
+* ``init_C2_<kind>.npz``  ``ray_initial_numpy`` rows + ``select_initial_step``   (wr.py:344-395, rkf45.py:34-99)
+* ``traj_C1.npz``       full C1 history through ``main_wr.real2d_hnf``          (main_wr.py:31-89)
+* ``traj_C2_<kind>.npz``  C2 history rows 1, 12, 120 (+ per-ray accepted steps)
+* ``roots_C3.npz``      initial rows on a C3 subsample (stationary, 10-day period)
+* ``kat_stepper.npz``   ``rk45_simple_current`` on the rkf45.py demo ODEs      (rkf45.py:672-724,825-882)
+"""
+import contextlib
+import hashlib
+import io
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.join(ROOT, "rossby-wave-ray-tracing_amd"))
+
+import refharness as H          # noqa: E402
+import synthetic as S           # noqa: E402
+
+R = H.load_reference()
+PI = R.constants.pi
+
+
+def quiet(fn, *a, **k):
+    with contextlib.redirect_stdout(io.StringIO()):
+        return fn(*a, **k)
+
+
+def make_wr(bg, cfg, name):
+    """A reference WR with its basic state ready (main_wr.py:66-86)."""
+    H.put_nc(name, **bg)
+    wr = R.wr.WR(cfg.nzwn, cfg.nsource, cfg.tstep * R.constants.hour,
+                 cfg.ttotal * R.constants.day, cfg.freq,
+                 nx=len(bg["lon"]), ny=len(bg["lat"]), rtol=cfg.rtol,
+                 atol=cfg.atol, ncfile=name, MinStepFactor=cfg.MinStepFactor)
+    wr.bs.loadbs_ncfile(name)
+    wr.bs.ready(xcyclic=True)
+    wr.set_zwn(cfg.zwn)
+    wr.set_source_matrix(cfg.SW_lon, cfg.SW_lat, cfg.dlon, cfg.dlat, cfg.nnx, cfg.nny)
+    return wr
+
+
+def fun_of(wr):
+    def fun(t, y):
+        return wr.diffun_numpy(y.reshape((5, -1, 1, 1)))[0][0:5].reshape((5, -1))
+    return fun
+
+
+def random_states(rng, n):
+    y = np.empty((5, n))
+    y[0] = rng.uniform(-3 * PI, 5 * PI, n)
+    y[1] = rng.uniform(-1.58, 1.58, n)
+    y[2] = rng.uniform(0.5, 12.0, n)
+    y[3] = rng.uniform(-110.0, 110.0, n)
+    y[4] = rng.uniform(0.1, 5.0, n)
+    return y
+
+
+def edge_states(bs):
+    """Hand-picked edge cases: poles, grid lines, mod-2pi seams, NaN, |l| = 100."""
+    rows = []
+    base = [2.0, 0.6, 5.0, 3.0, 1.0]
+    def add(**kw):
+        r = list(base)
+        for k, v in kw.items():
+            r["lon lat k l amp".split().index(k)] = v
+        rows.append(r)
+    for lat in [0.5 * PI, -0.5 * PI, np.nextafter(0.5 * PI, 0), -np.nextafter(0.5 * PI, 0),
+                1.5533, -1.5533, 1.56, -1.565, 0.0, -0.0]:
+        add(lat=lat)
+    for lon in [0.0, -0.0, 2 * PI, -1e-300, 2 * PI - 1e-15, 4 * PI, -2 * PI, 1e3, -1e3, 3649 * PI / 180]:
+        add(lon=lon)
+    for j in [0, 1, 35, 36, 71, 72]:
+        add(lat=bs.lat[j])
+    for i in [0, 1, 72, 143]:
+        add(lon=bs.lon[i])
+    add(lon=bs.lon[143] + 0.5 * (bs.lon[1] - bs.lon[0]))
+    for l in [100.0, -100.0, np.nextafter(100.0, 0), 99.99]:
+        add(l=l)
+    for k in [0.0, -3.0, 1e-8]:
+        add(k=k)
+    for v in range(5):
+        r = list(base)
+        r[v] = np.nan
+        rows.append(r)
+    add(amp=np.inf)
+    add(lon=np.inf)
+    return np.array(rows).T
+
+
+def hash_fields(f):
+    return hashlib.sha256(np.ascontiguousarray(f, dtype=np.float64).tobytes()).hexdigest()
+
+
+def gen_background(kind, rng):
+    bg = S.background(kind)
+    cfg = S.config("C2", bg=kind)
+    wr = make_wr(bg, cfg, f"bg_{kind}.nc")
+    bs = wr.bs
+    F = bs.fields
+    np.savez_compressed(os.path.join(HERE, f"bg_{kind}.npz"),
+                        sha256=np.array(hash_fields(F)), shape=np.array(F.shape),
+                        sample=F[::7, ::5, :], lat=bs.lat, lon=bs.lon)
+    # mercator point records
+    n = 2048
+    lon = np.concatenate([rng.uniform(-2 * PI, 4 * PI, n - 64), np.linspace(0, 2 * PI, 64)])
+    lat = np.concatenate([rng.uniform(-1.575, 1.575, n - 64), np.linspace(-0.5 * PI, 0.5 * PI, 64)])
+    M = bs.cal_bs_mercator_point(lon.copy(), lat.copy(), mode="numpy")
+    np.savez_compressed(os.path.join(HERE, f"merc_{kind}.npz"), lon=lon, lat=lat, out=M)
+    # RHS records
+    y = np.concatenate([random_states(rng, 4096 - 64), edge_states(bs)], axis=1)
+    y = y[:, :4096]
+    d, bad = wr.diffun_numpy(y.reshape((5, -1, 1, 1)).copy())
+    np.savez_compressed(os.path.join(HERE, f"rhs_{kind}.npz"), y=y,
+                        dydt=d[0:5].reshape(5, -1), bad=bad.reshape(-1))
+    # single-step records (realistic states: inside the domain, |l| moderate)
+    fun = fun_of(wr)
+    m = 1024
+    ys = random_states(rng, m)
+    ys[1] = rng.uniform(-1.3, 1.3, m)
+    ys[3] = rng.uniform(-20, 20, m)
+    f = fun(0, ys)
+    h = 10 ** rng.uniform(0.0, 4.5, m)
+    K = np.empty((7, 5, m))
+    t = np.zeros(m)
+    yn, _ = R.rkf45.rk_step(fun, t, ys, f, h, R.rkf45.RK45.A, R.rkf45.RK45.B,
+                            R.rkf45.RK45.C, K)
+    scale = 1e-6 + np.maximum(np.abs(ys), np.abs(yn)) * 1e-6
+    en = R.rkf45.norm(h[None, :] * np.einsum("snf,s->nf", K, R.rkf45.RK45.E) / scale)
+    np.savez_compressed(os.path.join(HERE, f"step_{kind}.npz"), y=ys, f=f, h=h,
+                        K=K, y_new=yn, err_norm=en)
+    # C2 initial rows + initial step
+    quiet(wr.ray_initial, mode="numpy", root_method="numpy")
+    rows = np.array([wr.rlon[0], wr.rlat[0], wr.rzwn[0], wr.rmwn[0], wr.ramp[0],
+                     wr.rug[0], wr.rvg[0]])
+    y0 = rows[:5].reshape(5, -1)
+    f0 = fun(0, y0)
+    h0 = R.rkf45.select_initial_step(fun, np.zeros(y0.shape[1]), y0, f0,
+                                     np.array([1.0]), 4, 1e-6, 1e-6)
+    np.savez_compressed(os.path.join(HERE, f"init_C2_{kind}.npz"), rows=rows, f0=f0, h_abs=h0)
+    return wr
+
+
+class StepCounter:
+    """Count accepted steps per column by wrapping RungeKutta._step_impl."""
+
+    def __init__(self):
+        self.orig = R.rkf45.RungeKutta._step_impl
+        self.nacc = None
+        self.attempts = 0
+        self.orig_rk_step = R.rkf45.rk_step
+
+    def __enter__(self):
+        me = self
+
+        def step_impl(solver):
+            y = solver.y
+            live = ~np.isnan(np.mean(y, axis=0)) & (solver.t != solver.t_bound)
+            if me.nacc is None:
+                me.nacc = np.zeros(y.shape[1], np.int64)
+            out = me.orig(solver)
+            me.nacc[live] += 1
+            return out
+
+        def rk_step(fun, t, *a, **k):
+            me.attempts += len(t)
+            return me.orig_rk_step(fun, t, *a, **k)
+
+        R.rkf45.RungeKutta._step_impl = step_impl
+        R.rkf45.rk_step = rk_step
+        return self
+
+    def __exit__(self, *a):
+        R.rkf45.RungeKutta._step_impl = self.orig
+        R.rkf45.rk_step = self.orig_rk_step
+
+
+def run_traj(kind, name, nt, rows_keep=None):
+    bg = S.background(kind)
+    cfg = S.config(name, bg=kind)
+    cfg.ttotal = (nt - 1) * cfg.tstep / 24.0
+    wr = make_wr(bg, cfg, f"traj_{name}_{kind}.nc")
+    t0 = time.time()
+    with StepCounter() as sc:
+        quiet(wr.ray_run, mode="numpy", inte_method="rk45", root_method="numpy")
+    dt = time.time() - t0
+    hist = np.array([wr.rlon, wr.rlat, wr.rzwn, wr.rmwn, wr.ramp, wr.rug, wr.rvg])
+    hist = hist.reshape(7, nt, -1)
+    keep = np.arange(nt) if rows_keep is None else np.asarray(rows_keep)
+    print(f"traj {name} {kind}: nt={nt} {dt:.1f}s accepted={sc.nacc.sum()} "
+          f"attempts={sc.attempts}")
+    return dict(rows=keep, hist=hist[:, keep], nacc=sc.nacc,
+                attempts=np.array(sc.attempts), nt=np.array(nt), wall=np.array(dt))
+
+
+def gen_roots():
+    """Initial rows on a C3 subsample: every 17th source, stationary and 10-day period."""
+    out = {}
+    for tag, period in [("stat", None), ("p10", 10.0)]:
+        for kind in ["zonal", "nonzonal"]:
+            bg = S.background(kind)
+            cfg = S.config("C3", period=period)
+            slon, slat = [], []
+            deg2rad = R.constants.deg2rad
+            for iy in range(cfg.nny):
+                for ix in range(cfg.nnx):
+                    if (iy * cfg.nnx + ix) % 17 == 0:
+                        slon.append(((cfg.SW_lon % 360.0 + ix * cfg.dlon) % 360.0))
+                        slat.append(cfg.SW_lat + iy * cfg.dlat)
+            H.put_nc("roots.nc", **bg)
+            wr = R.wr.WR(cfg.nzwn, len(slon), 7200.0, 7200.0, cfg.freq, nx=144, ny=73,
+                         ncfile="roots.nc")
+            wr.bs.loadbs_ncfile("roots.nc")
+            wr.bs.ready(xcyclic=True)
+            wr.set_zwn(cfg.zwn)
+            wr.set_source_array(slon, slat)
+            quiet(wr.ray_initial, mode="numpy", root_method="numpy")
+            out[f"{tag}_{kind}_src"] = np.array([wr.source_lon, wr.source_lat])
+            out[f"{tag}_{kind}_freq"] = np.array(cfg.freq)
+            out[f"{tag}_{kind}_rows"] = np.array([wr.rmwn[0], wr.ramp[0], wr.rug[0], wr.rvg[0]])
+    np.savez_compressed(os.path.join(HERE, "roots_C3.npz"), **out)
+
+
+def gen_kat():
+    rk = R.rkf45
+    out = {}
+    ts = np.linspace(0, 40, 4001)
+
+    def lin(t, u):
+        x, = u
+        return np.array([2 * t + x * 0])
+
+    def ex(t, u):
+        x, = u
+        return np.array([np.e ** (0.1 * t) + x * 0])
+
+    def lorenz(t, u, p=10, b=8 / 3, r=28):
+        x, y, z = u
+        return np.array([-p * x + p * y, -x * z + r * x - y, x * y - b * z])
+
+    y0 = np.array([[0.1], [0.2]]).T
+    out["lin_y0"] = y0
+    out["lin_ys"] = rk.rk45_simple_current(lin, (0, 40), y0, t_eval=ts)[1]
+    y0 = np.array([[10.0], [20.0]]).T
+    out["exp_y0"] = y0
+    out["exp_ys"] = rk.rk45_simple_current(ex, (0, 40), y0, t_eval=ts, rtol=1e-14, atol=1e-15)[1]
+    y0 = np.array([[0.1, 0.1, 0.1], [10, 8 / 3, 28]]).T
+    out["lorenz_y0"] = y0
+    out["lorenz_ys"] = rk.rk45_simple_current(lorenz, (0, 40), y0, t_eval=ts)[1]
+    out["t_eval"] = ts
+    np.savez_compressed(os.path.join(HERE, "kat_stepper.npz"), **out)
+
+
+def main():
+    rng = np.random.default_rng(20251015)
+    for kind in ["zonal", "nonzonal"]:
+        gen_background(kind, rng)
+        print("background", kind, "done")
+    c1 = run_traj("zonal", "C1", 1081)
+    np.savez_compressed(os.path.join(HERE, "traj_C1.npz"), **c1)
+    for kind in ["zonal", "nonzonal"]:
+        c2 = run_traj(kind, "C2", 121, rows_keep=[1, 12, 120])
+        np.savez_compressed(os.path.join(HERE, f"traj_C2_{kind}.npz"), **c2)
+    gen_roots()
+    gen_kat()
+    print("done")
+
+
+if __name__ == "__main__":
+    main()
