@@ -1,0 +1,202 @@
+"""Benchmark: RK45 ray-steps/s of the MI355X ray integrator (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--days D]
+
+One "step" = one pass of the hot path over one batch: the whole C3 workload
+(2-degree global seed grid x k = 1..10 x periods {inf, 50, 30, 20, 10} d =
+2.40 M ray slots, of which ~0.7 M have a real initial root) integrated for
+90 days (1081 output rows at 2 h) -- solver construction, the ray loop and
+every output row included.  Inputs are resident in HBM when the timed region
+starts.  For N > 1 each rank (one per GPU, launched by torch.distributed.run)
+integrates its own C3-sized batch (sources shifted by r*2/N degrees of
+longitude): per-GPU work is fixed, rays never interact, no collective runs
+inside the timed region (scaling "weak").
+
+Rank 0 prints ONE JSON line.  ``roofline`` prices the ray-loop kernel at the
+algorithmic 2112 B per accepted ray-step; ``cpu_baseline``
+times the NumPy oracle (oracle/rwrt_oracle.py, bit-exact with the reference)
+on a bounded sample of the same rays on the host.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "rossby-wave-ray-tracing_amd"))
+
+import torch  # noqa: E402
+
+import synthetic as S  # noqa: E402
+
+METRIC = "ray-steps/sec (whole node), 10^6 rays RKF45; max |Δpos| vs CPU ref"
+BYTES_PER_STEP = 2112          # 6 RHS evals x 4 corners x 11 fields x 8 B
+HBM_PEAK = 8.0e12              # MI355X_MICROARCH.md, chip-level parameters
+
+
+def c3_initial_state(bs, lon_offset_deg=0.0, periods=S.C3_PERIODS_DAYS):
+    """Initial ray state y0[5, nslot] of C3 (all periods concatenated)."""
+    from wr import initial_rows
+    cfg = S.config("C3")
+    deg2rad = np.pi / 180.0
+    ix, iy = np.meshgrid(np.arange(cfg.nnx), np.arange(cfg.nny))
+    lon = (((cfg.SW_lon + lon_offset_deg) % 360.0 + ix.ravel() * cfg.dlon) % 360.0) * deg2rad
+    lat = (cfg.SW_lat + iy.ravel() * cfg.dlat) * deg2rad
+    ys = []
+    for P in periods:
+        with np.errstate(all="ignore"):
+            rows = initial_rows(bs, lon, lat, cfg.zwn, S.c3_freq(P))
+        ys.append(np.array(rows[:5]).reshape(5, -1))
+    return np.concatenate(ys, axis=1)
+
+
+def make_bs(kind="zonal"):
+    from bs import BS
+    bg = S.background(kind)
+    bs = BS(len(bg["lon"]), len(bg["lat"]))
+    bs.load_arrays(**bg)
+    bs.ready(xcyclic=True)
+    return bs, bg
+
+
+def cpu_baseline(bg, y0, nrays, days, seed=0):
+    """Time the oracle on ``nrays`` live rays for ``days`` (1 host core)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import rwrt_oracle as O
+    rng = np.random.default_rng(seed)
+    live = np.where(~np.isnan(y0.mean(axis=0)))[0]
+    pick = np.sort(rng.choice(live, size=min(nrays, len(live)), replace=False))
+    ob = O.Background(**bg)
+    nt = int(round(days * 12)) + 1
+    t0 = time.perf_counter()
+    with np.errstate(all="ignore"):
+        hist, nacc, nrej, st = O.ray_run(ob, y0[:, pick].copy(), nt, 7200.0)
+    dt = time.perf_counter() - t0
+    return pick, hist, int(nacc.sum()), dt, nt
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--days", type=float, default=90.0, help="integration horizon per step")
+    ap.add_argument("--chunk", type=int, default=0, help="output rows per kernel launch")
+    ap.add_argument("--cpu-rays", type=int, default=16384)
+    ap.add_argument("--cpu-days", type=float, default=4.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--periods", type=int, default=5, help="C3 periods in the batch (1-5)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    dev = torch.device("cuda", local if world > 1 else 0)
+
+    from engine import RayEngine
+    bs, bg = make_bs("zonal")
+    t_init = time.perf_counter()
+    y0 = c3_initial_state(bs, lon_offset_deg=rank * 2.0 / max(world, 1),
+                          periods=S.C3_PERIODS_DAYS[: args.periods])
+    t_init = time.perf_counter() - t_init
+    nslot = y0.shape[1]
+    n_live = int(np.sum(~np.isnan(y0.mean(axis=0))))
+    eng = RayEngine.from_bs(bs, device=dev)
+    y0_d = torch.as_tensor(y0, device=dev)
+    nt = int(round(args.days * 12)) + 1
+    chunk = args.chunk or max(1, min(nt - 1, (8 << 30) // (nslot * 64)))
+    out = torch.empty((nslot, min(chunk, nt - 1), 8), dtype=torch.float64, device=dev)
+
+    def one_step(events=None):
+        return eng.integrate(y0_d, nt, 7200.0, ttotal=(nt - 1) * 7200.0, chunk=chunk, out=out,
+                             events=events)
+
+    for _ in range(args.warmup):
+        one_step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    events, steps_done = [], 0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        r = one_step(events)
+        steps_done += r.ray_steps
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_s = sum(a.elapsed_time(b) for a, b in events) / 1e3
+    rej = int(r.nrej.sum().item())
+
+    tot_steps, max_el = steps_done, elapsed
+    if dist:
+        t = torch.tensor([float(steps_done), elapsed], dtype=torch.float64, device=dev)
+        s = t.clone()
+        dist.all_reduce(s, op=dist.ReduceOp.SUM)
+        m = t.clone()
+        dist.all_reduce(m, op=dist.ReduceOp.MAX)
+        tot_steps, max_el = s[0].item(), m[1].item()
+
+    result = None
+    if rank == 0:
+        value = tot_steps / max_el
+        per_launch_steps = steps_done / max(len(events), 1)
+        avg_launch_s = kern_s / max(len(events), 1)
+        achieved = per_launch_steps * BYTES_PER_STEP / avg_launch_s
+        result = {
+            "metric": METRIC, "value": value, "unit": "ray-steps/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": 1e3 * max_el / args.steps, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "config": {"workload": f"C3: 2deg global seeds x k=1..10 x {args.periods} periods, "
+                                   f"{args.days:g} d at 2 h, 2.5deg DJF jet background (BASELINE configs[2])",
+                       "ray_slots_per_gpu": nslot, "live_rays_per_gpu": n_live, "rows": nt,
+                       "rows_per_launch": chunk, "parallelism": f"rays sharded, {world} rank(s), 1 GPU each"},
+            "ray_steps_per_step": steps_done / args.steps,
+            "rejected_per_accepted": rej / max(r.ray_steps, 1),
+            "host_init_s": t_init,
+            "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK, "traffic": None,
+                         "kernel": "rk45_run_kernel", "avg_launch_ms": 1e3 * avg_launch_s,
+                         "launches": len(events), "bytes_per_ray_step": BYTES_PER_STEP},
+        }
+        if world == 1 and not args.no_cpu:
+            pick, hist, csteps, cdt, cnt = cpu_baseline(bg, y0, args.cpu_rays, args.cpu_days)
+            result["cpu_baseline"] = {
+                "value": csteps / cdt, "unit": "ray-steps/s", "cores": 1, "kind": "port",
+                "sample": f"{len(pick)} live C3 rays x {args.cpu_days:g} d ({csteps} ray-steps, "
+                          f"{cdt:.1f} s) with oracle/rwrt_oracle.py (NumPy, bit-exact vs reference)",
+                "host_cpus": os.cpu_count()}
+            # parity of the same sample on the GPU after the same horizon
+            rows = {}
+            eng.integrate(torch.as_tensor(y0[:, pick], device=dev), cnt, 7200.0,
+                          sink=lambda a, b, o: rows.__setitem__(a, o[:, :, :2].cpu().numpy()))
+            gpu = np.concatenate([rows[k] for k in sorted(rows)], axis=1)   # rows 1..cnt-1
+            parity = []
+            for row in sorted({min(12, cnt - 1), cnt - 1}):
+                g, c = gpu[:, row - 1], hist[:2, row].T
+                ok = ~np.isnan(g).any(1) & ~np.isnan(c).any(1)
+                d = np.max(np.abs(g[ok] - c[ok]), axis=1) if ok.any() else np.zeros(1)
+                parity.append({"horizon_days": row / 12.0, "rays": int(ok.sum()),
+                               "p50": float(np.median(d)), "p99": float(np.percentile(d, 99)),
+                               "max": float(d.max()),
+                               "alive_mismatch": int(np.sum(np.isnan(g[:, 0]) != np.isnan(c[:, 0])))})
+            result["max_dpos_vs_cpu_rad"] = parity
+        print(json.dumps(result))
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

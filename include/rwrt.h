@@ -1,0 +1,141 @@
+/*
+ * rwrt.h -- C ABI of the MI355X batched Rossby-wave ray integrator.
+ *
+ * The reference (yinan-codes/Rossby-wave-ray-tracing) has no FFI: its ray loop
+ * is selected by Python method dispatch, WR.ray_run -> WR.core_ray_run
+ * ('numpy_rk45') -> WR.core_ray_run_rk45 (wr.py:889-911, 767-887).  The
+ * entry points below are what that dispatch binds instead (ctypes, see
+ * INTEGRATION.md); each cites the reference function it replaces.
+ *
+ * Conventions
+ *  - Every pointer named d_* is DEVICE memory owned by the caller (the Python
+ *    host keeps it in PyTorch-ROCm tensors).  The library never allocates or
+ *    frees caller memory.
+ *  - All calls are asynchronous and ordered on `stream` (a hipStream_t; NULL =
+ *    the default stream).  Status codes report argument and launch errors;
+ *    per-ray failure is data (NaN), exactly as in the reference.
+ *  - fp64 throughout; the fields are the reference's 18-field stack.
+ */
+#ifndef RWRT_H
+#define RWRT_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RWRT_ABI_VERSION 1
+#define RWRT_NFIELD_REF 18  /* BS.fields[..., 18]            (bs.py:349-368) */
+#define RWRT_NFIELD_PACK 12 /* 11 hot fields + 1 pad per grid point           */
+#define RWRT_NVAR 5         /* y = (lon, lat, k, l, amp)     (wr.py:768-776)  */
+#define RWRT_NMERC 12       /* fmu .. fmqyy                  (bs.py:885-887)  */
+#define RWRT_NOUT 8         /* per output row: lon lat k l amp ug vg nacc     */
+#define RWRT_NSTATE 12      /* per ray: y[5] f[5] t h_abs                     */
+
+typedef enum {
+  RWRT_OK = 0,
+  RWRT_ERR_ARG = 1,        /* bad argument (message in rwrt_last_error)     */
+  RWRT_ERR_HIP = 2,        /* HIP launch / runtime error                     */
+  RWRT_SOLVER_FAILED = 3   /* rkf45.py:423-425 "All nan" (set by the host)   */
+} rwrt_status;
+
+/* Grid of BS.fields: W = nlon (+1 cyclic pad column, bs.py:370-372) columns,
+ * H = nlat rows.  lon0/dlon, lat0/dlat are bs.lon[0], bs.lon[1]-bs.lon[0],
+ * bs.lat[0], bs.lat[1]-bs.lat[0] of the float32-rounded grid
+ * (bs.py:225-236, interpolation.py:78-82). */
+typedef struct {
+  int32_t ncol;
+  int32_t nrow;
+  double lon0, dlon;
+  double lat0, dlat;
+} rwrt_grid;
+
+/* Solver parameters of WR.core_ray_run_rk45 / RK45 (wr.py:792-794). */
+typedef struct {
+  double rtol;      /* max(rtol, 100 eps)          rkf45.py:21-26  */
+  double atol;
+  double min_step;  /* Global_Minstep              rkf45.py:362    */
+  double cut_off;   /* jump mask threshold, rad    wr.py:170       */
+  int32_t nt;       /* rows of the history         wr.py:157       */
+  int32_t reserved;
+} rwrt_params;
+
+const char* rwrt_version(void);
+/* Last error message of the calling thread ("" if none). */
+const char* rwrt_last_error(void);
+
+/* Device layout of BS.fields (bs.py:349-372): d_fields is the reference stack
+ * [ncol][nrow][18] fp64; d_packed receives [ncol][nrow][12] (the 11 fields the
+ * hot path reads -- u v ux uy vx vy qx qy qxx qxy qyy -- plus a zero pad). */
+rwrt_status rwrt_pack_fields(const rwrt_grid* g, const double* d_fields,
+                             double* d_packed, void* stream);
+
+/* BS.cal_bs_mercator_point(lon, lat, mode='numpy') (bs.py:513-519,781-887):
+ * d_out[12][n] = fmu fmv fmux fmuy fmvx fmvy fmqx fmqy fmqxx fmqxy fmqyx fmqyy. */
+rwrt_status rwrt_mercator_point(const rwrt_grid* g, const double* d_packed,
+                                int64_t n, const double* d_lon,
+                                const double* d_lat, double* d_out,
+                                void* stream);
+
+/* WR.diffun_numpy(y)[0][0:5] (wr.py:492-556 with core_diffun wr.py:44-82 and
+ * cal_ugvg 'extent' wn.py:266-294): d_y[5][n] -> d_dydt[5][n]. */
+rwrt_status rwrt_rhs(const rwrt_grid* g, const double* d_packed, int64_t n,
+                     const double* d_y, double* d_dydt, void* stream);
+
+/* One Dormand-Prince 5(4) attempt: rk_step (rkf45.py:259-321) followed by
+ * _estimate_error_norm (rkf45.py:368-373, scale rkf45.py:442-445).
+ * d_y, d_f: [5][n]; d_h: [n] (signed step).  Outputs d_K[7][5][n],
+ * d_ynew[5][n], d_err[n] (NaN kept, as the reference returns it). */
+rwrt_status rwrt_dp54_attempt(const rwrt_grid* g, const double* d_packed,
+                              int64_t n, const double* d_y, const double* d_f,
+                              const double* d_h, double rtol, double atol,
+                              double* d_K, double* d_ynew, double* d_err,
+                              void* stream);
+
+/* Solver construction: RungeKutta.__init__ (rkf45.py:335-366) with
+ * select_initial_step (rkf45.py:34-99) on d_y0[5][nray].
+ * Writes d_state[12][nray] = y f t(=0) h_abs, zeroes d_count[nray][2]
+ * (accepted, rejected), sets d_nanrow[nray] = nt and d_live[nray] (1 if the
+ * ray's state has a finite mean, rkf45.py:400-403).  d_summary[2] (int64,
+ * zeroed here) accumulates {live rays, live rays with a finite h_abs}: the
+ * host raises RWRT_SOLVER_FAILED when the first is > 0 and the second is 0
+ * (the only way rkf45.py:423-425 can trigger). */
+rwrt_status rwrt_rk45_init(const rwrt_grid* g, const double* d_packed,
+                           int64_t nray, const double* d_y0,
+                           const rwrt_params* p, double* d_state,
+                           int64_t* d_count, int32_t* d_nanrow,
+                           int32_t* d_live, int64_t* d_summary, void* stream);
+
+/* The ray loop WR.core_ray_run_rk45 (wr.py:767-887) for output rows
+ * it_begin <= i < it_end (1 <= it_begin < it_end <= nt): every ray is stepped
+ * to d_tbound[i] (t_eval, wr.py:798-801) with the reference's step control
+ * (rkf45.py:222-253,375-514), then masked (wr.py:838-850) and its group
+ * velocity recomputed (wr.py:856-865).  Rays are taken from a device work
+ * queue in the order d_order[nray] (NULL = 0..nray-1).  Output row r of ray j
+ * is d_out[(j*(it_end-it_begin) + r)*8 + {lon,lat,k,l,amp,ug,vg,nacc}].
+ * d_state / d_count / d_nanrow carry the per-ray solver state across calls
+ * (time chunking).  d_work: >= 1 int32 of scratch (the queue head), reset by
+ * this call on `stream`. */
+rwrt_status rwrt_rk45_run(const rwrt_grid* g, const double* d_packed,
+                          int64_t nray, const rwrt_params* p,
+                          const double* d_tbound, int32_t it_begin,
+                          int32_t it_end, const int64_t* d_order,
+                          double* d_state, int64_t* d_count,
+                          int32_t* d_nanrow, double* d_out, int32_t* d_work,
+                          void* stream);
+
+/* Stepper known-answer tests: the same device stepper on the analytic ODEs of
+ * the rkf45.py demos (rkf45.py:839-882), driven like rk45_simple_current
+ * (rkf45.py:672-724).  kind: 0 dx/dt = 2t, 1 dx/dt = e^(0.1 t), 2 Lorenz
+ * (nvar 1, 1, 3).  d_y0[nvar][ncol]; d_teval[nt]; d_out[ncol][nt][nvar]. */
+rwrt_status rwrt_kat_rk45(int32_t kind, int64_t ncol, const double* d_y0,
+                          int32_t nt, const double* d_teval, double rtol,
+                          double atol, double min_step, double* d_out,
+                          void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RWRT_H */

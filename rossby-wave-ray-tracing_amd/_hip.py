@@ -1,0 +1,109 @@
+"""ctypes binding of librwrt.so (the C ABI declared in include/rwrt.h).
+
+PyTorch-ROCm owns every device buffer: callers pass tensors, this module
+passes ``data_ptr()`` and the current HIP stream.  There is no CPU fallback:
+if the library is missing or no GPU is visible, every entry point raises.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  -- load torch's HIP runtime first (same SONAME as ours)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("RWRT_LIB", os.path.join(_HERE, "librwrt.so"))
+
+NFIELD_REF, NFIELD_PACK, NVAR, NMERC, NOUT, NSTATE = 18, 12, 5, 12, 8, 12
+ABI_SYMBOLS = ("rwrt_version", "rwrt_last_error", "rwrt_pack_fields",
+               "rwrt_mercator_point", "rwrt_rhs", "rwrt_dp54_attempt",
+               "rwrt_rk45_init", "rwrt_rk45_run", "rwrt_kat_rk45")
+
+RWRT_OK, RWRT_ERR_ARG, RWRT_ERR_HIP, RWRT_SOLVER_FAILED = 0, 1, 2, 3
+
+
+class RwrtError(RuntimeError):
+    pass
+
+
+class SolverFailed(RwrtError):
+    """rkf45.py:423-425: every retrying column has a NaN step (status -1)."""
+
+
+class Grid(ctypes.Structure):
+    _fields_ = [("ncol", ctypes.c_int32), ("nrow", ctypes.c_int32),
+                ("lon0", ctypes.c_double), ("dlon", ctypes.c_double),
+                ("lat0", ctypes.c_double), ("dlat", ctypes.c_double)]
+
+
+class Params(ctypes.Structure):
+    _fields_ = [("rtol", ctypes.c_double), ("atol", ctypes.c_double),
+                ("min_step", ctypes.c_double), ("cut_off", ctypes.c_double),
+                ("nt", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+_lib = None
+_P = ctypes.c_void_p
+_I64 = ctypes.c_int64
+_I32 = ctypes.c_int32
+_D = ctypes.c_double
+
+
+def load():
+    """Load librwrt.so (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RwrtError(f"HIP library not found at {LIB_PATH}: build it with "
+                        f"`make -C rossby-wave-ray-tracing_amd/csrc` (hipcc, gfx950)")
+    lib = ctypes.CDLL(LIB_PATH)
+    lib.rwrt_version.restype = ctypes.c_char_p
+    lib.rwrt_last_error.restype = ctypes.c_char_p
+    G, Pr = ctypes.POINTER(Grid), ctypes.POINTER(Params)
+    sig = {
+        "rwrt_pack_fields": [G, _P, _P, _P],
+        "rwrt_mercator_point": [G, _P, _I64, _P, _P, _P, _P],
+        "rwrt_rhs": [G, _P, _I64, _P, _P, _P],
+        "rwrt_dp54_attempt": [G, _P, _I64, _P, _P, _P, _D, _D, _P, _P, _P, _P],
+        "rwrt_rk45_init": [G, _P, _I64, _P, Pr, _P, _P, _P, _P, _P, _P],
+        "rwrt_rk45_run": [G, _P, _I64, Pr, _P, _I32, _I32, _P, _P, _P, _P, _P, _P, _P],
+        "rwrt_kat_rk45": [_I32, _I64, _P, _I32, _P, _D, _D, _D, _P, _P],
+    }
+    for name, args in sig.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = ctypes.c_int
+    _lib = lib
+    return lib
+
+
+def version():
+    return load().rwrt_version().decode()
+
+
+def check(status):
+    if status != RWRT_OK:
+        msg = load().rwrt_last_error().decode()
+        raise RwrtError(f"rwrt status {status}: {msg}")
+
+
+def require_gpu():
+    if not torch.cuda.is_available():
+        raise RwrtError("no HIP device visible: the ray integrator runs only on the GPU "
+                        "(there is no CPU fallback)")
+
+
+def dptr(t, dtype=None, what="tensor"):
+    """Device pointer of a contiguous tensor (checked)."""
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise RwrtError(f"{what} must be a device tensor")
+    if dtype is not None and t.dtype != dtype:
+        raise RwrtError(f"{what} must be {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise RwrtError(f"{what} must be contiguous")
+    return t.data_ptr()
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream

@@ -1,0 +1,870 @@
+// rwrt.hip -- fused RK45 Rossby-wave ray integrator for MI355X (gfx950).
+//
+// One lane owns one ray for a whole time chunk: Dormand-Prince 5(4) stages,
+// the dispersion-relation RHS (bilinear gather of the basic state, Mercator
+// conversion, group velocity, wavenumber/amplitude tendencies), per-ray
+// adaptive step control, the per-interval masks and the output rows all run
+// in registers.  Lanes pull rays from a device work queue so that a lane whose
+// ray finishes early immediately starts another one (the 4.6x spread of steps
+// per ray would otherwise idle most of every wavefront).
+//
+// Numerics follow the reference operation by operation (built with
+// -ffp-contract=off, IEEE division and sqrt): every expression keeps the
+// reference's evaluation order.  Reference file:line in each comment.
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "rwrt.h"
+
+namespace rwrt {
+
+// constants.py:13-16
+constexpr double kPi = 3.14159265358979323846;
+constexpr double kHalfPi = 0.5 * kPi;  // "0.5 * pi"  wr.py:508, bs.py:787
+constexpr double kTwoPi = 2.0 * kPi;   // "2 * pi"    bs.py:519, interpolation.py:80
+constexpr double kREarth = 6.3712e6;
+constexpr double kNaN = __builtin_nan("");
+
+// rkf45.py:604-615 (Dormand-Prince 5(4)); C++ constant division is IEEE
+// correctly rounded, like Python's.
+constexpr double kC[6] = {0.0, 1.0 / 5, 3.0 / 10, 4.0 / 5, 8.0 / 9, 1.0};
+constexpr double kA[6][5] = {
+    {0, 0, 0, 0, 0},
+    {1.0 / 5, 0, 0, 0, 0},
+    {3.0 / 40, 9.0 / 40, 0, 0, 0},
+    {44.0 / 45, -56.0 / 15, 32.0 / 9, 0, 0},
+    {19372.0 / 6561, -25360.0 / 2187, 64448.0 / 6561, -212.0 / 729, 0},
+    {9017.0 / 3168, -355.0 / 33, 46732.0 / 5247, 49.0 / 176, -5103.0 / 18656}};
+constexpr double kB[6] = {35.0 / 384, 0, 500.0 / 1113, 125.0 / 192, -2187.0 / 6784, 11.0 / 84};
+constexpr double kE[7] = {-71.0 / 57600, 0, 71.0 / 16695, -71.0 / 1920,
+                          17253.0 / 339200, -22.0 / 525, 1.0 / 40};
+constexpr double kSafety = 0.9, kMinFactor = 0.2, kMaxFactor = 10.0;  // rkf45.py:363-366
+constexpr double kErrExp = -0.2;  // -1 / (error_estimator_order + 1)   rkf45.py:360
+
+// x.shape[0] ** 0.5 in rkf45.norm (rkf45.py:31), per number of variables.
+template <int NV> struct RootN;
+template <> struct RootN<1> { static constexpr double v = 1.0; };
+template <> struct RootN<3> { static constexpr double v = 1.7320508075688772; };
+template <> struct RootN<5> { static constexpr double v = 2.23606797749979; };
+
+// ---------------------------------------------------------------------------
+// NumPy element semantics
+// ---------------------------------------------------------------------------
+// np.maximum / np.minimum: NaN-propagating.
+__device__ __forceinline__ double np_max(double a, double b) {
+  return (a >= b || a != a) ? a : b;
+}
+__device__ __forceinline__ double np_min(double a, double b) {
+  return (a <= b || a != a) ? a : b;
+}
+// Python/NumPy floor modulo for float64 (npy_remainder): fmod, then move a
+// remainder whose sign differs from b into [0, b); exact zero gets b's sign.
+__device__ __forceinline__ double py_mod(double a, double b) {
+  double m = fmod(a, b);
+  if (m != 0.0) {
+    if ((b < 0.0) != (m < 0.0)) m += b;
+  } else {
+    m = copysign(0.0, b);
+  }
+  return m;
+}
+// np.floor(x).astype('int32') on x86-64: out-of-range and NaN give INT32_MIN.
+__device__ __forceinline__ int64_t floor_i32(double x) {
+  double f = floor(x);
+  if (!(f >= -2147483648.0 && f <= 2147483647.0)) return -2147483648LL;
+  return (int64_t)f;
+}
+__device__ __forceinline__ int clip(int64_t v, int hi) {
+  return (int)(v < 0 ? 0 : (v > hi ? hi : v));
+}
+
+// ---------------------------------------------------------------------------
+// Basic state: packed [W][H][12] fp64, the 11 hot fields of BS.fields
+// ---------------------------------------------------------------------------
+enum { F_U = 0, F_V, F_UX, F_UY, F_VX, F_VY, F_QX, F_QY, F_QXX, F_QXY, F_QYY, F_PAD };
+constexpr int kNF = RWRT_NFIELD_PACK;
+// slot -> index in the reference 18-field stack (bs.py:349-368); qyx (10) and
+// the six third derivatives are never read on the hot path.
+__constant__ int kRefIndex[11] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 11};
+
+struct Field {
+  const double* __restrict__ P;
+  int W, H;
+  double lon0, dlon, lat0, dlat;
+};
+
+// Bilinear corner set + weights of batch_linint2_metpy/bilinear_interpolation_
+// (interpolation.py:77-85, 103-135) for one in-range point.
+struct Corners {
+  const double* a;  // F[x0, y1]
+  const double* b;  // F[x1, y1]
+  const double* c;  // F[x0, y0]
+  const double* d;  // F[x1, y0]
+  double wa, wb, wc, wd;
+};
+
+__device__ __forceinline__ Corners corners(const Field& F, double lon, double lat) {
+  // lon arrives already reduced once (bs.py:519); interpolation.py:80 reduces again.
+  const double lons = py_mod(lon, kTwoPi);
+  const double x = (lons - F.lon0) / F.dlon;
+  const double y = (lat - F.lat0) / F.dlat;
+  const int64_t ix = floor_i32(x), iy = floor_i32(y);
+  const int x0 = clip(ix, F.W - 1), x1 = clip(ix + 1, F.W - 1);
+  const int y0 = clip(iy, F.H - 1), y1 = clip(iy + 1, F.H - 1);
+  const double sx = x - (double)x0, sy = y - (double)y0;
+  Corners k;
+  k.a = F.P + ((size_t)x0 * F.H + y1) * kNF;
+  k.b = F.P + ((size_t)x1 * F.H + y1) * kNF;
+  k.c = F.P + ((size_t)x0 * F.H + y0) * kNF;
+  k.d = F.P + ((size_t)x1 * F.H + y0) * kNF;
+  k.wa = (1.0 - sx) * sy;
+  k.wb = sx * sy;
+  k.wc = (1.0 - sx) * (1.0 - sy);
+  k.wd = sx * (1.0 - sy);
+  return k;
+}
+
+// a*wa + b*wb + c*wc + d*wd, left to right (interpolation.py:132-133)
+__device__ __forceinline__ double blend(const Corners& k, double a, double b, double c, double d) {
+  return ((a * k.wa + b * k.wb) + c * k.wc) + d * k.wd;
+}
+
+// Interpolate all 11 hot fields (NaN outside |lat| <= pi/2, bs.py:787,822-836).
+__device__ __forceinline__ void interp11(const Field& F, double lon, double lat, double g[11]) {
+  if (!(fabs(lat) <= kHalfPi)) {
+#pragma unroll
+    for (int i = 0; i < 11; ++i) g[i] = kNaN;
+    return;
+  }
+  const Corners k = corners(F, lon, lat);
+  const double2* pa = reinterpret_cast<const double2*>(k.a);
+  const double2* pb = reinterpret_cast<const double2*>(k.b);
+  const double2* pc = reinterpret_cast<const double2*>(k.c);
+  const double2* pd = reinterpret_cast<const double2*>(k.d);
+#pragma unroll
+  for (int q = 0; q < 6; ++q) {
+    const double2 va = pa[q], vb = pb[q], vc = pc[q], vd = pd[q];
+    g[2 * q] = blend(k, va.x, vb.x, vc.x, vd.x);
+    if (2 * q + 1 < 11) g[2 * q + 1] = blend(k, va.y, vb.y, vc.y, vd.y);
+  }
+}
+
+// Only u, v, qx, qy (what cal_ugvg needs, wr.py:856-865).
+__device__ __forceinline__ void interp4(const Field& F, double lon, double lat,
+                                        double& fu, double& fv, double& fqx, double& fqy) {
+  if (!(fabs(lat) <= kHalfPi)) {
+    fu = fv = fqx = fqy = kNaN;
+    return;
+  }
+  const Corners k = corners(F, lon, lat);
+  const double2 a0 = *reinterpret_cast<const double2*>(k.a + F_U);
+  const double2 b0 = *reinterpret_cast<const double2*>(k.b + F_U);
+  const double2 c0 = *reinterpret_cast<const double2*>(k.c + F_U);
+  const double2 d0 = *reinterpret_cast<const double2*>(k.d + F_U);
+  const double2 a1 = *reinterpret_cast<const double2*>(k.a + F_QX);
+  const double2 b1 = *reinterpret_cast<const double2*>(k.b + F_QX);
+  const double2 c1 = *reinterpret_cast<const double2*>(k.c + F_QX);
+  const double2 d1 = *reinterpret_cast<const double2*>(k.d + F_QX);
+  fu = blend(k, a0.x, b0.x, c0.x, d0.x);
+  fv = blend(k, a0.y, b0.y, c0.y, d0.y);
+  fqx = blend(k, a1.x, b1.x, c1.x, d1.x);
+  fqy = blend(k, a1.y, b1.y, c1.y, d1.y);
+}
+
+// Mercator factors of cal_bs_mercator_point (bs.py:856-860).
+struct Merc {
+  double c, s, m, cp;
+};
+__device__ __forceinline__ Merc merc_factors(double lat, double c, double s) {
+  Merc r;
+  r.c = c;
+  r.s = s;
+  r.m = (fabs(c) <= 0.0175) ? 0.0 : 1.0;
+  r.cp = c * r.m + (1.0 - r.m) * 1e-6;
+  return r;
+}
+
+// The 12 Mercator outputs the hot path uses (bs.py:862-883), in the order of
+// the returned stack: fmu fmv fmux fmuy fmvx fmvy fmqx fmqy fmqxx fmqxy fmqyx fmqyy.
+__device__ __forceinline__ void mercator12(const double g[11], const Merc& M, double t, double o[12]) {
+  const double m = M.m, cp = M.cp;
+  const double fu = g[F_U], fv = g[F_V];
+  o[0] = (fu / cp) * m;                                      // fmu
+  o[1] = (fv / cp) * m;                                      // fmv
+  o[2] = (g[F_UX] / cp) * m;                                 // fmux
+  o[3] = (g[F_UY] + t * fu) * m;                             // fmuy
+  o[4] = (g[F_VX] / cp) * m;                                 // fmvx
+  o[5] = (g[F_VY] + t * fv) * m;                             // fmvy
+  o[6] = g[F_QX] * m;                                        // fmqx
+  o[7] = (g[F_QY] * cp) * m;                                 // fmqy
+  o[8] = g[F_QXX] * m;                                       // fmqxx
+  o[10] = (g[F_QXY] * cp) * m;                               // fmqyx
+  o[9] = o[10] * m;                                          // fmqxy = fmqyx * mask
+  o[11] = (((g[F_QYY] * cp) - (g[F_QY] * M.s)) * cp) * m;    // fmqyy
+}
+
+// cal_ugvg(mode='extent') -> core_cal_ugvg_extent (wn.py:266-294)
+__device__ __forceinline__ void ugvg(double fu, double fv, double fqx, double fqy,
+                                     double k, double l, double& ug, double& vg) {
+  const double kap = l / k;
+  const double kap2 = kap * kap;
+  const double kap1 = 1.0 + kap2;
+  const double KK = (k * k) * kap1;
+  const double denom = KK * kap1;
+  ug = fu + (((1.0 - kap2) * fqy) - ((2.0 * kap) * fqx)) / denom;
+  vg = fv + (((2.0 * kap) * fqy) + ((1.0 - kap2) * fqx)) / denom;
+}
+
+// ---------------------------------------------------------------------------
+// The RHS: WR.diffun_numpy (wr.py:492-556) + core_diffun (wr.py:44-82)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void ray_rhs(const Field& F, const double* y, double* dy) {
+  const double lon = y[0], lat = y[1], kx = y[2], ky = y[3], amp = y[4];
+  // wr.py:508-514 -- a masked ray returns NaN for every derivative (wr.py:552-553)
+  if (fabs(lat) >= kHalfPi || fabs(ky) >= 100.0) {
+#pragma unroll
+    for (int v = 0; v < 5; ++v) dy[v] = kNaN;
+    return;
+  }
+  double g[11];
+  interp11(F, py_mod(lon, kTwoPi), lat, g);
+  const double c = cos(lat), s = sin(lat), tn = tan(lat);
+  const Merc M = merc_factors(lat, c, s);
+  double o[12];
+  mercator12(g, M, tn, o);
+  const double fmu = o[0], fmv = o[1], fmux = o[2], fmuy = o[3], fmvx = o[4], fmvy = o[5];
+  const double fmqx = o[6], fmqy = o[7], fmqxx = o[8], fmqxy = o[9], fmqyx = o[10], fmqyy = o[11];
+  double ug, vg;
+  ugvg(fmu, fmv, fmqx, fmqy, kx, ky, ug, vg);
+  // core_diffun (wr.py:53-78); freq only feeds the dead ps/up terms
+  const double kap = ky / kx;
+  const double kap2 = kap * kap;
+  const double kap1 = 1.0 + kap * kap;
+  const double kk = (kx * kx) * kap1;
+  const double dzwn = (-kx) * ((fmux + kap * fmvx) + (kap * fmqxx - fmqyx) / kk);
+  const double dmwn = (-kx) * ((fmuy + kap * fmvy) + (kap * fmqxy - fmqyy) / kk);
+  const double damp1 = (2.0 * ((fmux + fmvy) + kap * (fmvx + fmuy))) / kap1;
+  const double damp2 = (2.0 * (kap * (fmqxx - fmqyy) + (kap2 - 1.0) * fmqxy)) / (kk * kap1);
+  const double damp3 = (-2.0 * s) * fmv;
+  const double damp = (damp1 + damp2) + damp3;
+  dy[0] = ug / kREarth;
+  dy[1] = (vg * c) / kREarth;
+  dy[2] = dzwn / kREarth;
+  dy[3] = dmwn / kREarth;
+  dy[4] = (damp * amp) / kREarth;
+}
+
+// group velocity at a stored position (wr.py:856-865): no |l| mask here
+__device__ __forceinline__ void ugvg_at(const Field& F, double lon, double lat, double k,
+                                        double l, double& ug, double& vg) {
+  double fu, fv, fqx, fqy;
+  interp4(F, py_mod(lon, kTwoPi), lat, fu, fv, fqx, fqy);
+  const double c = cos(lat);
+  const double m = (fabs(c) <= 0.0175) ? 0.0 : 1.0;
+  const double cp = c * m + (1.0 - m) * 1e-6;
+  ugvg((fu / cp) * m, (fv / cp) * m, fqx * m, (fqy * cp) * m, k, l, ug, vg);
+}
+
+// cal_dis (wr.py:97-112): haversine between consecutive stored positions
+__device__ __forceinline__ double cal_dis(double lon_c, double lat_c, double lon_p, double lat_p) {
+  const double sd = sin((lat_c - lat_p) / 2.0);
+  const double sl = sin((lon_c - lon_p) / 2.0);
+  const double a = sd * sd + (cos(lat_p) * cos(lat_c)) * (sl * sl);
+  return fabs(2.0 * atan2(sqrt(a), sqrt(1.0 - a)));
+}
+
+// ---------------------------------------------------------------------------
+// Problems the stepper integrates
+// ---------------------------------------------------------------------------
+struct RayProblem {
+  static constexpr int NV = 5;
+  static constexpr bool kAutonomous = true;  // fun ignores t (wr.py:784-789)
+  Field F;
+  __device__ __forceinline__ void operator()(double, const double* y, double* dy) const {
+    ray_rhs(F, y, dy);
+  }
+};
+
+// rkf45.py demo ODEs (rkf45.py:775-782, 839-841, 861-863)
+struct KatLinear {
+  static constexpr int NV = 1;
+  static constexpr bool kAutonomous = false;
+  __device__ void operator()(double t, const double* y, double* dy) const { dy[0] = 2.0 * t + y[0] * 0.0; }
+};
+struct KatExp {
+  static constexpr int NV = 1;
+  static constexpr bool kAutonomous = false;
+  __device__ void operator()(double t, const double* y, double* dy) const {
+    dy[0] = pow(2.718281828459045, 0.1 * t) + y[0] * 0.0;  // np.e ** (0.1 * t)
+  }
+};
+struct KatLorenz {
+  static constexpr int NV = 3;
+  static constexpr bool kAutonomous = false;
+  __device__ void operator()(double, const double* u, double* d) const {
+    const double p = 10.0, b = 8.0 / 3, r = 28.0;
+    const double x = u[0], y = u[1], z = u[2];
+    d[0] = (-p) * x + p * y;
+    d[1] = ((-x) * z + r * x) - y;
+    d[2] = x * y - b * z;
+  }
+};
+
+// ---------------------------------------------------------------------------
+// Dormand-Prince 5(4) attempt, rk_step (rkf45.py:259-321) + error norm
+// ---------------------------------------------------------------------------
+// np.einsum('snf,s->nf', K[:S], w) in NumPy's order: sequential in s for more
+// than one variable; for one variable einsum's 2-lane SIMD dot product sums the
+// even and the odd terms separately (oracle/rwrt_oracle.py wsum).
+template <int NV, int S>
+__device__ __forceinline__ double wsum(const double (&K)[7][NV], const double* w, int v) {
+  if constexpr (NV == 1) {
+    double even = 0.0, odd = 0.0;
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      if (j % 2 == 0) even = even + K[j][v] * w[j];
+      else odd = odd + K[j][v] * w[j];
+    }
+    return even + odd;
+  } else {
+    double acc = 0.0;
+#pragma unroll
+    for (int j = 0; j < S; ++j) acc = acc + K[j][v] * w[j];
+    return acc;
+  }
+}
+
+template <int S, int NV>
+__device__ __forceinline__ void stage_point(const double (&K)[7][NV], const double* y, double h,
+                                            double* ys) {
+#pragma unroll
+  for (int v = 0; v < NV; ++v) ys[v] = y[v] + wsum<NV, S>(K, kA[S], v) * h;
+}
+
+// Returns the error norm (NaN kept); fills y_new and K.
+template <class P>
+__device__ __forceinline__ double dp54_attempt(const P& fun, double t, const double* y,
+                                               const double* f, double h, double rtol,
+                                               double atol, double (&K)[7][P::NV],
+                                               double* ynew) {
+  constexpr int NV = P::NV;
+  double ys[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) K[0][v] = f[v];
+  stage_point<1>(K, y, h, ys);
+  fun(t + kC[1] * h, ys, K[1]);
+  stage_point<2>(K, y, h, ys);
+  fun(t + kC[2] * h, ys, K[2]);
+  stage_point<3>(K, y, h, ys);
+  fun(t + kC[3] * h, ys, K[3]);
+  stage_point<4>(K, y, h, ys);
+  fun(t + kC[4] * h, ys, K[4]);
+  stage_point<5>(K, y, h, ys);
+  fun(t + kC[5] * h, ys, K[5]);
+#pragma unroll
+  for (int v = 0; v < NV; ++v) ynew[v] = y[v] + h * wsum<NV, 6>(K, kB, v);
+  fun(t + h, ynew, K[6]);
+  // _estimate_error_norm: norm(h * (E . K) / scale), scale = atol + max(|y|,|y_new|) rtol
+  double ss = 0.0;
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const double e = h * wsum<NV, 7>(K, kE, v);
+    const double sc = atol + np_max(fabs(y[v]), fabs(ynew[v])) * rtol;
+    const double x = e / sc;
+    ss = (v == 0) ? x * x : ss + x * x;
+  }
+  return sqrt(ss) / RootN<NV>::v;
+}
+
+// select_initial_step (rkf45.py:34-99), direction = +1
+template <class P>
+__device__ __forceinline__ double initial_step(const P& fun, double t0, const double* y0,
+                                               const double* f0, double rtol, double atol) {
+  constexpr int NV = P::NV;
+  double sc[NV], y1[NV], f1[NV];
+  double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    sc[v] = atol + fabs(y0[v]) * rtol;
+    const double a = y0[v] / sc[v], b = f0[v] / sc[v];
+    s0 = (v == 0) ? a * a : s0 + a * a;
+    s1 = (v == 0) ? b * b : s1 + b * b;
+  }
+  const double d0 = sqrt(s0) / RootN<NV>::v, d1 = sqrt(s1) / RootN<NV>::v;
+  double h0 = (0.01 * d0) / d1;
+  if (d0 < 1e-5) h0 = 1e-6;
+  if (d1 < 1e-5) h0 = 1e-6;
+#pragma unroll
+  for (int v = 0; v < NV; ++v) y1[v] = y0[v] + h0 * f0[v];
+  fun(t0 + h0, y1, f1);
+  double s2 = 0.0;
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const double a = (f1[v] - f0[v]) / sc[v];
+    s2 = (v == 0) ? a * a : s2 + a * a;
+  }
+  const double d2 = (sqrt(s2) / RootN<NV>::v) / h0;
+  double h1;
+  if (!(d1 > 1e-15) && !(d2 > 1e-15)) {
+    h1 = np_max(1e-6, h0 * 1e-3);
+  } else {
+    const double dm = (d1 != d1) ? d2 : ((d2 != d2) ? d1 : (d1 >= d2 ? d1 : d2));  // nanmax
+    h1 = pow(0.01 / dm, 0.2);
+  }
+  return np_min(100.0 * h0, h1);
+}
+
+// One lane's solver: the per-column part of OdeSolver.step / _step_impl
+// (rkf45.py:222-253, 375-514).  iterate() runs at most ONE attempt and
+// reports whether the column reached t_bound.
+template <class P>
+struct Lane {
+  static constexpr int NV = P::NV;
+  double y[NV], f[NV];
+  double t, habs, hs;
+  bool in_step, rejected;
+
+  __device__ __forceinline__ bool iterate(const P& fun, double tb, double min_step, double rtol,
+                                          double atol, int64_t& nacc, int64_t& nrej) {
+    if (!in_step) {
+      double sum = y[0];
+#pragma unroll
+      for (int v = 1; v < NV; ++v) sum = sum + y[v];
+      if (isnan(sum / (double)NV)) {  // NaN mean: frozen, t := t_bound (rkf45.py:400-403)
+        t = tb;
+        return true;
+      }
+      if (t == tb) return true;
+      if (!P::kAutonomous) fun(t, y, f);   // rkf45.py:378 (equal to K6 if autonomous)
+      hs = np_max(habs, min_step);         // rkf45.py:383-387
+      rejected = false;
+      in_step = true;
+    }
+    double h = hs;                          // h_abs * direction
+    double tn = t + h;
+    if (tn - tb > 0.0) tn = tb;             // rkf45.py:429
+    h = tn - t;
+    const double ha = fabs(h);
+    double K[7][NV], yn[NV];
+    double en = dp54_attempt(fun, t, y, f, h, rtol, atol, K, yn);
+    if (en != en) en = 0.0;                 // rkf45.py:446
+    if (en < 1.0) {
+      double fac = np_min(kMaxFactor, kSafety * pow(en, kErrExp));
+      if (en == 0.0) fac = kMaxFactor;
+      if (rejected) fac = np_min(1.0, fac);
+      habs = ha * fac;
+      t = (tn != tn) ? tb : tn;             // rkf45.py:503
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {
+        y[v] = yn[v];
+        f[v] = K[6][v];
+      }
+      in_step = false;
+      ++nacc;
+      return t - tb >= 0.0;                 // rkf45.py:250
+    }
+    hs = ha * np_max(kMinFactor, kSafety * pow(en, kErrExp));
+    rejected = true;
+    ++nrej;
+    return false;
+  }
+};
+
+// ---------------------------------------------------------------------------
+// Kernels
+// ---------------------------------------------------------------------------
+__global__ void pack_fields_kernel(const double* __restrict__ ref, double* __restrict__ out,
+                                   int64_t npts) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= npts) return;
+  const double* src = ref + i * RWRT_NFIELD_REF;
+  double* dst = out + i * kNF;
+#pragma unroll
+  for (int q = 0; q < 11; ++q) dst[q] = src[kRefIndex[q]];
+  dst[F_PAD] = 0.0;
+}
+
+__global__ void mercator_kernel(Field F, int64_t n, const double* __restrict__ lon,
+                                const double* __restrict__ lat, double* __restrict__ out) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const double la = lat[i];
+    double g[11], o[12];
+    interp11(F, py_mod(lon[i], kTwoPi), la, g);
+    const Merc M = merc_factors(la, cos(la), sin(la));
+    mercator12(g, M, tan(la), o);
+#pragma unroll
+    for (int q = 0; q < 12; ++q) out[q * n + i] = o[q];
+  }
+}
+
+__global__ void rhs_kernel(Field F, int64_t n, const double* __restrict__ y,
+                           double* __restrict__ dydt) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    double yy[5], d[5];
+#pragma unroll
+    for (int v = 0; v < 5; ++v) yy[v] = y[v * n + i];
+    ray_rhs(F, yy, d);
+#pragma unroll
+    for (int v = 0; v < 5; ++v) dydt[v * n + i] = d[v];
+  }
+}
+
+__global__ void attempt_kernel(Field F, int64_t n, const double* __restrict__ y,
+                               const double* __restrict__ f, const double* __restrict__ h,
+                               double rtol, double atol, double* __restrict__ Kout,
+                               double* __restrict__ ynew, double* __restrict__ err) {
+  const RayProblem P{F};
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    double yy[5], ff[5], K[7][5], yn[5];
+#pragma unroll
+    for (int v = 0; v < 5; ++v) {
+      yy[v] = y[v * n + i];
+      ff[v] = f[v * n + i];
+    }
+    err[i] = dp54_attempt(P, 0.0, yy, ff, h[i], rtol, atol, K, yn);
+#pragma unroll
+    for (int v = 0; v < 5; ++v) ynew[v * n + i] = yn[v];
+#pragma unroll
+    for (int s = 0; s < 7; ++s)
+#pragma unroll
+      for (int v = 0; v < 5; ++v) Kout[(s * 5 + v) * n + i] = K[s][v];
+  }
+}
+
+struct InitArgs {
+  Field F;
+  int64_t nray;
+  const double* y0;
+  double rtol, atol;
+  int32_t nt;
+  double* state;
+  int64_t* count;
+  int32_t* nanrow;
+  int32_t* live;
+  int64_t* summary;
+};
+
+__global__ void rk45_init_kernel(InitArgs a) {
+  const RayProblem P{a.F};
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < a.nray;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    double y[5], f[5];
+#pragma unroll
+    for (int v = 0; v < 5; ++v) y[v] = a.y0[v * a.nray + i];
+    P(0.0, y, f);                                   // RungeKutta.__init__: f = fun(t, y)
+    const double habs = initial_step(P, 0.0, y, f, a.rtol, a.atol);
+#pragma unroll
+    for (int v = 0; v < 5; ++v) {
+      a.state[v * a.nray + i] = y[v];
+      a.state[(5 + v) * a.nray + i] = f[v];
+    }
+    a.state[10 * a.nray + i] = 0.0;
+    a.state[11 * a.nray + i] = habs;
+    a.count[2 * i] = 0;
+    a.count[2 * i + 1] = 0;
+    a.nanrow[i] = a.nt;
+    const double mean = ((((y[0] + y[1]) + y[2]) + y[3]) + y[4]) / 5.0;
+    const bool live = !isnan(mean);
+    a.live[i] = live ? 1 : 0;
+    if (live) {
+      atomicAdd(reinterpret_cast<unsigned long long*>(&a.summary[0]), 1ull);
+      if (!isnan(habs)) atomicAdd(reinterpret_cast<unsigned long long*>(&a.summary[1]), 1ull);
+    }
+  }
+}
+
+struct RunArgs {
+  Field F;
+  int64_t nray;
+  double rtol, atol, min_step, cut_off;
+  int32_t nt, it_begin, it_end;
+  const double* tbound;
+  const int64_t* order;
+  double* state;
+  int64_t* count;
+  int32_t* nanrow;
+  double* out;
+  int32_t* queue;
+};
+
+// WR.core_ray_run_rk45 (wr.py:767-887) for rows [it_begin, it_end): persistent
+// lanes, one ray each, refilled from the work queue.
+__global__ void __launch_bounds__(256) rk45_run_kernel(RunArgs a) {
+  const RayProblem P{a.F};
+  const int64_t nrows = a.it_end - a.it_begin;
+  Lane<RayProblem> L;
+  int64_t ray = -1, nacc = 0, nrej = 0;
+  int32_t it = 0, nanrow = 0;
+  double prev_lon = 0.0, prev_lat = 0.0;
+  for (;;) {
+    if (ray < 0) {
+      const int32_t w = atomicAdd(a.queue, 1);
+      if (w >= a.nray) break;
+      ray = a.order ? a.order[w] : (int64_t)w;
+#pragma unroll
+      for (int v = 0; v < 5; ++v) {
+        L.y[v] = a.state[v * a.nray + ray];
+        L.f[v] = a.state[(5 + v) * a.nray + ray];
+      }
+      L.t = a.state[10 * a.nray + ray];
+      L.habs = a.state[11 * a.nray + ray];
+      L.in_step = false;
+      L.rejected = false;
+      L.hs = 0.0;
+      nacc = a.count[2 * ray];
+      nrej = a.count[2 * ray + 1];
+      nanrow = a.nanrow[ray];
+      it = a.it_begin;
+      prev_lon = L.y[0];   // == rlon[it-1], rlat[it-1] (wr.py:844, 877-885)
+      prev_lat = L.y[1];
+    }
+    const double tb = a.tbound[it];
+    if (!L.iterate(P, tb, a.min_step, a.rtol, a.atol, nacc, nrej)) continue;
+
+    // ---- interval it reached: post-processing (wr.py:835-885) ----
+    double* y = L.y;
+    if (fabs(y[1]) >= kHalfPi) {
+#pragma unroll
+      for (int v = 0; v < 5; ++v) y[v] = kNaN;
+    }
+    if (cal_dis(y[0], y[1], prev_lon, prev_lat) >= a.cut_off) {
+#pragma unroll
+      for (int v = 0; v < 5; ++v) y[v] = kNaN;
+    }
+    double ug, vg;
+    ugvg_at(a.F, y[0], y[1], y[2], y[3], ug, vg);
+    double2* o = reinterpret_cast<double2*>(a.out + ((size_t)ray * nrows + (it - a.it_begin)) * RWRT_NOUT);
+    o[0] = make_double2(y[0], y[1]);
+    o[1] = make_double2(y[2], y[3]);
+    o[2] = make_double2(y[4], ug);
+    o[3] = make_double2(vg, (double)nacc);
+    prev_lon = y[0];
+    prev_lat = y[1];
+    if (nanrow == a.nt && isnan(y[0])) nanrow = it;  // wr.py:853-855 (host reduces)
+    if (++it == a.it_end) {
+#pragma unroll
+      for (int v = 0; v < 5; ++v) {
+        a.state[v * a.nray + ray] = y[v];
+        a.state[(5 + v) * a.nray + ray] = L.f[v];
+      }
+      a.state[10 * a.nray + ray] = L.t;
+      a.state[11 * a.nray + ray] = L.habs;
+      a.count[2 * ray] = nacc;
+      a.count[2 * ray + 1] = nrej;
+      a.nanrow[ray] = nanrow;
+      ray = -1;
+    }
+  }
+}
+
+// rk45_simple_current (rkf45.py:672-724) over ncol columns, one lane each.
+template <class P>
+__global__ void kat_kernel(int64_t ncol, const double* __restrict__ y0, int32_t nt,
+                           const double* __restrict__ teval, double rtol, double atol,
+                           double min_step, double* __restrict__ out) {
+  constexpr int NV = P::NV;
+  const P fun{};
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= ncol) return;
+  Lane<P> L;
+#pragma unroll
+  for (int v = 0; v < NV; ++v) L.y[v] = y0[v * ncol + i];
+  L.t = teval[0];
+  fun(L.t, L.y, L.f);
+  L.habs = initial_step(fun, L.t, L.y, L.f, rtol, atol);
+  L.in_step = false;
+  L.rejected = false;
+  int64_t nacc = 0, nrej = 0;
+  for (int v = 0; v < NV; ++v) out[(i * nt) * NV + v] = L.y[v];
+  for (int it = 1; it < nt; ++it) {
+    while (!L.iterate(fun, teval[it], min_step, rtol, atol, nacc, nrej)) {
+    }
+    for (int v = 0; v < NV; ++v) out[(i * nt + it) * NV + v] = L.y[v];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Host side of the ABI
+// ---------------------------------------------------------------------------
+thread_local std::string g_err;
+
+rwrt_status fail(rwrt_status s, const char* fmt, const char* detail = "") {
+  char buf[512];
+  snprintf(buf, sizeof buf, fmt, detail);
+  g_err = buf;
+  return s;
+}
+
+rwrt_status check_launch(const char* what) {
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    g_err = std::string(what) + ": " + hipGetErrorString(e);
+    return RWRT_ERR_HIP;
+  }
+  return RWRT_OK;
+}
+
+rwrt_status make_field(const rwrt_grid* g, const double* packed, Field& F) {
+  if (!g) return fail(RWRT_ERR_ARG, "grid is NULL%s");
+  if (!packed) return fail(RWRT_ERR_ARG, "packed fields pointer is NULL%s");
+  if (g->ncol < 2 || g->nrow < 2) return fail(RWRT_ERR_ARG, "grid must be at least 2x2%s");
+  if (!(g->dlon != 0.0) || !(g->dlat != 0.0)) return fail(RWRT_ERR_ARG, "grid spacing is zero%s");
+  if (reinterpret_cast<uintptr_t>(packed) % 16 != 0)
+    return fail(RWRT_ERR_ARG, "packed fields must be 16-byte aligned%s");
+  F.P = packed;
+  F.W = g->ncol;
+  F.H = g->nrow;
+  F.lon0 = g->lon0;
+  F.dlon = g->dlon;
+  F.lat0 = g->lat0;
+  F.dlat = g->dlat;
+  return RWRT_OK;
+}
+
+unsigned grid_for(int64_t n, int block) {
+  int64_t b = (n + block - 1) / block;
+  if (b < 1) b = 1;
+  if (b > 65535LL * 32) b = 65535LL * 32;
+  return (unsigned)b;
+}
+
+int persistent_blocks() {
+  static int cached = 0;
+  if (cached) return cached;
+  int dev = 0, ncu = 0, per = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 1024;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) ncu = 256;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(rk45_run_kernel),
+                                                   256, 0) != hipSuccess || per < 1)
+    per = 1;
+  cached = ncu * per;
+  return cached;
+}
+
+}  // namespace rwrt
+
+using namespace rwrt;
+
+extern "C" {
+
+const char* rwrt_version(void) { return "rwrt 0.1 (gfx950, abi 1)"; }
+
+const char* rwrt_last_error(void) { return g_err.c_str(); }
+
+rwrt_status rwrt_pack_fields(const rwrt_grid* g, const double* d_fields, double* d_packed,
+                             void* stream) {
+  if (!g || !d_fields || !d_packed) return fail(RWRT_ERR_ARG, "NULL argument to rwrt_pack_fields%s");
+  const int64_t npts = (int64_t)g->ncol * g->nrow;
+  hipLaunchKernelGGL(pack_fields_kernel, dim3(grid_for(npts, 256)), dim3(256), 0,
+                     (hipStream_t)stream, d_fields, d_packed, npts);
+  return check_launch("pack_fields_kernel");
+}
+
+rwrt_status rwrt_mercator_point(const rwrt_grid* g, const double* d_packed, int64_t n,
+                                const double* d_lon, const double* d_lat, double* d_out,
+                                void* stream) {
+  Field F;
+  if (rwrt_status s = make_field(g, d_packed, F)) return s;
+  if (n < 0 || (n > 0 && (!d_lon || !d_lat || !d_out))) return fail(RWRT_ERR_ARG, "bad point arrays%s");
+  if (n == 0) return RWRT_OK;
+  hipLaunchKernelGGL(mercator_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, F,
+                     n, d_lon, d_lat, d_out);
+  return check_launch("mercator_kernel");
+}
+
+rwrt_status rwrt_rhs(const rwrt_grid* g, const double* d_packed, int64_t n, const double* d_y,
+                     double* d_dydt, void* stream) {
+  Field F;
+  if (rwrt_status s = make_field(g, d_packed, F)) return s;
+  if (n < 0 || (n > 0 && (!d_y || !d_dydt))) return fail(RWRT_ERR_ARG, "bad state arrays%s");
+  if (n == 0) return RWRT_OK;
+  hipLaunchKernelGGL(rhs_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, F, n,
+                     d_y, d_dydt);
+  return check_launch("rhs_kernel");
+}
+
+rwrt_status rwrt_dp54_attempt(const rwrt_grid* g, const double* d_packed, int64_t n,
+                              const double* d_y, const double* d_f, const double* d_h,
+                              double rtol, double atol, double* d_K, double* d_ynew,
+                              double* d_err, void* stream) {
+  Field F;
+  if (rwrt_status s = make_field(g, d_packed, F)) return s;
+  if (n < 0 || (n > 0 && (!d_y || !d_f || !d_h || !d_K || !d_ynew || !d_err)))
+    return fail(RWRT_ERR_ARG, "bad attempt arrays%s");
+  if (n == 0) return RWRT_OK;
+  hipLaunchKernelGGL(attempt_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, F,
+                     n, d_y, d_f, d_h, rtol, atol, d_K, d_ynew, d_err);
+  return check_launch("attempt_kernel");
+}
+
+rwrt_status rwrt_rk45_init(const rwrt_grid* g, const double* d_packed, int64_t nray,
+                           const double* d_y0, const rwrt_params* p, double* d_state,
+                           int64_t* d_count, int32_t* d_nanrow, int32_t* d_live,
+                           int64_t* d_summary, void* stream) {
+  Field F;
+  if (rwrt_status s = make_field(g, d_packed, F)) return s;
+  if (!p) return fail(RWRT_ERR_ARG, "params is NULL%s");
+  if (nray < 0 || nray > 0x7fffffffLL) return fail(RWRT_ERR_ARG, "nray out of range%s");
+  if (!d_y0 || !d_state || !d_count || !d_nanrow || !d_live || !d_summary)
+    return fail(RWRT_ERR_ARG, "NULL buffer to rwrt_rk45_init%s");
+  if (hipMemsetAsync(d_summary, 0, 2 * sizeof(int64_t), (hipStream_t)stream) != hipSuccess)
+    return check_launch("hipMemsetAsync(summary)");
+  if (nray == 0) return RWRT_OK;
+  InitArgs a{F, nray, d_y0, p->rtol, p->atol, p->nt, d_state, d_count, d_nanrow, d_live, d_summary};
+  hipLaunchKernelGGL(rk45_init_kernel, dim3(grid_for(nray, 256)), dim3(256), 0,
+                     (hipStream_t)stream, a);
+  return check_launch("rk45_init_kernel");
+}
+
+rwrt_status rwrt_rk45_run(const rwrt_grid* g, const double* d_packed, int64_t nray,
+                          const rwrt_params* p, const double* d_tbound, int32_t it_begin,
+                          int32_t it_end, const int64_t* d_order, double* d_state,
+                          int64_t* d_count, int32_t* d_nanrow, double* d_out, int32_t* d_work,
+                          void* stream) {
+  Field F;
+  if (rwrt_status s = make_field(g, d_packed, F)) return s;
+  if (!p) return fail(RWRT_ERR_ARG, "params is NULL%s");
+  if (nray < 0 || nray > 0x7fffffffLL) return fail(RWRT_ERR_ARG, "nray out of range%s");
+  if (it_begin < 1 || it_end > p->nt || it_begin >= it_end)
+    return fail(RWRT_ERR_ARG, "need 1 <= it_begin < it_end <= nt%s");
+  if (!d_tbound || !d_state || !d_count || !d_nanrow || !d_out || !d_work)
+    return fail(RWRT_ERR_ARG, "NULL buffer to rwrt_rk45_run%s");
+  if (reinterpret_cast<uintptr_t>(d_out) % 16 != 0)
+    return fail(RWRT_ERR_ARG, "output rows must be 16-byte aligned%s");
+  if (nray == 0) return RWRT_OK;
+  if (hipMemsetAsync(d_work, 0, sizeof(int32_t), (hipStream_t)stream) != hipSuccess)
+    return check_launch("hipMemsetAsync(queue)");
+  RunArgs a{F, nray, p->rtol, p->atol, p->min_step, p->cut_off, p->nt, it_begin, it_end,
+            d_tbound, d_order, d_state, d_count, d_nanrow, d_out, d_work};
+  int64_t blocks = persistent_blocks();
+  const int64_t need = (nray + 255) / 256;
+  if (blocks > need) blocks = need;
+  hipLaunchKernelGGL(rk45_run_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
+  return check_launch("rk45_run_kernel");
+}
+
+rwrt_status rwrt_kat_rk45(int32_t kind, int64_t ncol, const double* d_y0, int32_t nt,
+                          const double* d_teval, double rtol, double atol, double min_step,
+                          double* d_out, void* stream) {
+  if (ncol <= 0 || nt < 1 || !d_y0 || !d_teval || !d_out) return fail(RWRT_ERR_ARG, "bad KAT arguments%s");
+  const dim3 grid(grid_for(ncol, 64)), block(64);
+  hipStream_t s = (hipStream_t)stream;
+  switch (kind) {
+    case 0: hipLaunchKernelGGL(kat_kernel<KatLinear>, grid, block, 0, s, ncol, d_y0, nt, d_teval, rtol, atol, min_step, d_out); break;
+    case 1: hipLaunchKernelGGL(kat_kernel<KatExp>, grid, block, 0, s, ncol, d_y0, nt, d_teval, rtol, atol, min_step, d_out); break;
+    case 2: hipLaunchKernelGGL(kat_kernel<KatLorenz>, grid, block, 0, s, ncol, d_y0, nt, d_teval, rtol, atol, min_step, d_out); break;
+    default: return fail(RWRT_ERR_ARG, "unknown KAT kind%s");
+  }
+  return check_launch("kat_kernel");
+}
+
+}  // extern "C"

@@ -1,0 +1,207 @@
+"""Device-side ray engine: the basic state resident in HBM + the HIP entry points.
+
+``RayEngine`` is what ``WR.core_ray_run_hip_rk45`` (wr.py) and ``bench.py``
+drive.  It owns the packed field stack on the GPU and wraps every C-ABI call
+of ``include/rwrt.h``; ``integrate`` is the whole ray loop of the reference's
+``WR.core_ray_run_rk45`` (wr.py:767-887), streamed in time chunks.
+"""
+import numpy as np
+import torch
+
+import _hip as H
+
+F64 = torch.float64
+
+
+def grid_of(lon, lat, ncol):
+    """``rwrt_grid`` from the float32-rounded radian axes (interpolation.py:78-82)."""
+    lon = np.asarray(lon, np.float64)
+    lat = np.asarray(lat, np.float64)
+    return H.Grid(int(ncol), len(lat), float(lon[0]), float(lon[1] - lon[0]),
+                  float(lat[0]), float(lat[1] - lat[0]))
+
+
+def t_eval_of(nt, tstep, ttotal=None):
+    """Output times ``arange(nt) * tstep`` clipped to ``ttotal`` (wr.py:798-801)."""
+    t = np.arange(nt) * np.float64(tstep)
+    if ttotal is not None and t[-1] > ttotal:
+        t[-1] = ttotal
+    return t
+
+
+class RunResult:
+    """Per-ray counters and the two global outcomes of one integration."""
+
+    def __init__(self, nacc, nrej, nanrow, failed, break_row, n_live):
+        self.nacc = nacc            # accepted steps per ray (torch int64, device)
+        self.nrej = nrej            # rejected attempts per ray
+        self.nanrow = nanrow        # first stored row with NaN lon per ray (nt = never)
+        self.failed = failed        # rkf45.py:423-425 -> wr.py:886-887
+        self.break_row = break_row  # wr.py:853-855 global early exit (None = no break)
+        self.n_live = n_live
+
+    @property
+    def ray_steps(self):
+        return int(self.nacc.sum().item())
+
+
+class RayEngine:
+    """The basic state on one GPU and the fused RK45 kernels that read it."""
+
+    def __init__(self, fields, lon, lat, device=None):
+        """``fields``: the reference stack ``[nlon(+1), nlat, 18]`` (numpy or tensor);
+        ``lon, lat``: the BS radian axes (``bs.lon``, ``bs.lat``)."""
+        H.require_gpu()
+        H.load()
+        self.device = torch.device(device or "cuda")
+        f = torch.as_tensor(np.ascontiguousarray(fields, dtype=np.float64)) \
+            if not torch.is_tensor(fields) else fields.to(F64)
+        if f.ndim != 3 or f.shape[-1] != H.NFIELD_REF:
+            raise ValueError(f"fields must be [ncol, nrow, {H.NFIELD_REF}], got {tuple(f.shape)}")
+        f = f.to(self.device).contiguous()
+        self.grid = grid_of(lon, lat, f.shape[0])
+        self.packed = torch.empty((f.shape[0], f.shape[1], H.NFIELD_PACK), dtype=F64,
+                                  device=self.device)
+        H.check(H.load().rwrt_pack_fields(self.grid, H.dptr(f), H.dptr(self.packed), H.stream()))
+        self.work = torch.zeros(4, dtype=torch.int32, device=self.device)
+
+    @classmethod
+    def from_bs(cls, bs, device=None):
+        return cls(bs.fields, bs.lon, bs.lat, device)
+
+    # ------------------------------------------------------------------ T0/T1
+    def mercator_point(self, lon, lat):
+        """``cal_bs_mercator_point`` on the GPU: ``(12, n)`` (fmu .. fmqyy)."""
+        lon = torch.as_tensor(lon, dtype=F64, device=self.device).contiguous()
+        lat = torch.as_tensor(lat, dtype=F64, device=self.device).contiguous()
+        n = lon.numel()
+        out = torch.empty((H.NMERC, n), dtype=F64, device=self.device)
+        H.check(H.load().rwrt_mercator_point(self.grid, H.dptr(self.packed), n, H.dptr(lon),
+                                             H.dptr(lat), H.dptr(out), H.stream()))
+        return out
+
+    def rhs(self, y):
+        """``diffun_numpy(y)[0][0:5]`` on the GPU for ``y[5, n]``."""
+        y = torch.as_tensor(y, dtype=F64, device=self.device).contiguous()
+        n = y.shape[1]
+        out = torch.empty_like(y)
+        H.check(H.load().rwrt_rhs(self.grid, H.dptr(self.packed), n, H.dptr(y), H.dptr(out),
+                                  H.stream()))
+        return out
+
+    def attempt(self, y, f, h, rtol=1e-6, atol=1e-6):
+        """One DP5(4) attempt (``rk_step`` + error norm): ``(K[7,5,n], y_new, err)``."""
+        y = torch.as_tensor(y, dtype=F64, device=self.device).contiguous()
+        f = torch.as_tensor(f, dtype=F64, device=self.device).contiguous()
+        h = torch.as_tensor(h, dtype=F64, device=self.device).contiguous()
+        n = y.shape[1]
+        K = torch.empty((7, 5, n), dtype=F64, device=self.device)
+        yn = torch.empty_like(y)
+        err = torch.empty(n, dtype=F64, device=self.device)
+        H.check(H.load().rwrt_dp54_attempt(self.grid, H.dptr(self.packed), n, H.dptr(y),
+                                           H.dptr(f), H.dptr(h), rtol, atol, H.dptr(K),
+                                           H.dptr(yn), H.dptr(err), H.stream()))
+        return K, yn, err
+
+    # ------------------------------------------------------------ ray loop
+    @staticmethod
+    def params(nt, tstep, rtol=1e-6, atol=1e-6, msf=1e-3, cut_off=0.1, cut_rad=None):
+        """``rwrt_params`` exactly as WR / RK45 derive them."""
+        rtol = max(rtol, 100 * np.finfo(np.float64).eps)          # rkf45.py:21-26
+        tstep = float(tstep)
+        min_step = min(msf * tstep, (tstep - 0) * 0.001)          # rkf45.py:362, wr.py:792-794
+        cut = cut_off * tstep / 3600.0 if cut_rad is None else float(cut_rad)   # wr.py:170
+        return H.Params(rtol, atol, min_step, cut, int(nt), 0)
+
+    def init(self, y0, p):
+        """Solver construction on the GPU; returns the per-ray state tensors."""
+        y0 = torch.as_tensor(y0, dtype=F64, device=self.device).contiguous()
+        nray = y0.shape[1]
+        st = dict(
+            state=torch.empty((H.NSTATE, nray), dtype=F64, device=self.device),
+            count=torch.empty((nray, 2), dtype=torch.int64, device=self.device),
+            nanrow=torch.empty(nray, dtype=torch.int32, device=self.device),
+            live=torch.empty(nray, dtype=torch.int32, device=self.device),
+            summary=torch.zeros(2, dtype=torch.int64, device=self.device),
+            nray=nray)
+        H.check(H.load().rwrt_rk45_init(self.grid, H.dptr(self.packed), nray, H.dptr(y0),
+                                        ctypes_ref(p), H.dptr(st["state"]), H.dptr(st["count"]),
+                                        H.dptr(st["nanrow"]), H.dptr(st["live"]),
+                                        H.dptr(st["summary"]), H.stream()))
+        return st
+
+    @staticmethod
+    def live_first_order(st):
+        """Queue order: live rays first, frozen (NaN-root) slots last (stable)."""
+        dead = (st["live"] == 0).to(torch.int8)
+        return torch.sort(dead, stable=True).indices.to(torch.int64).contiguous()
+
+    def run(self, st, p, tbound, it_begin, it_end, out, order=None):
+        """Rows ``[it_begin, it_end)`` into ``out[nray, it_end-it_begin, 8]`` (async)."""
+        H.check(H.load().rwrt_rk45_run(
+            self.grid, H.dptr(self.packed), st["nray"], ctypes_ref(p), H.dptr(tbound, F64),
+            int(it_begin), int(it_end), H.dptr(order, torch.int64), H.dptr(st["state"]),
+            H.dptr(st["count"]), H.dptr(st["nanrow"]), H.dptr(out, F64), H.dptr(self.work),
+            H.stream()))
+
+    def integrate(self, y0, nt, tstep, rtol=1e-6, atol=1e-6, msf=1e-3, cut_off=0.1,
+                  ttotal=None, chunk=None, sink=None, out=None, cut_rad=None, events=None):
+        """The whole ray loop for ``y0[5, nray]``; rows 1..nt-1 go to ``sink``.
+
+        ``sink(i0, i1, rows)`` receives each time chunk as a device tensor
+        ``rows[nray, i1-i0, 8]`` (lon lat k l amp ug vg nacc) before the next
+        chunk overwrites it.  ``events`` (a list) collects a pair of timing
+        events around every ray-loop launch.  Returns a ``RunResult``.
+        """
+        p = self.params(nt, tstep, rtol, atol, msf, cut_off, cut_rad)
+        y0 = torch.as_tensor(y0, dtype=F64, device=self.device).contiguous()
+        nray = y0.shape[1]
+        tb = torch.as_tensor(t_eval_of(nt, tstep, ttotal), dtype=F64, device=self.device)
+        st = self.init(y0, p)
+        summary = st["summary"].cpu()
+        n_live, n_finite = int(summary[0]), int(summary[1])
+        cnt = st["count"]
+        if n_live > 0 and n_finite == 0:
+            # rkf45.py:423-425: at the first step every live column has a NaN
+            # h_abs -> status -1 -> wr.py:886-887 breaks before storing row 1.
+            return RunResult(cnt[:, 0], cnt[:, 1], st["nanrow"], True, 1, n_live)
+        order = self.live_first_order(st)
+        chunk = chunk or (nt - 1)
+        if out is None or out.shape[0] != nray or out.shape[1] < min(chunk, nt - 1):
+            out = torch.empty((nray, min(chunk, nt - 1), H.NOUT), dtype=F64, device=self.device)
+        for i0 in range(1, nt, chunk):
+            i1 = min(i0 + chunk, nt)
+            view = out[:, : i1 - i0] if i1 - i0 < out.shape[1] else out
+            if not view.is_contiguous():
+                view = torch.empty((nray, i1 - i0, H.NOUT), dtype=F64, device=self.device)
+            if events is not None:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                self.run(st, p, tb, i0, i1, view, order)
+                e1.record()
+                events.append((e0, e1))
+            else:
+                self.run(st, p, tb, i0, i1, view, order)
+            if sink is not None:
+                sink(i0, i1, view)
+        mx = int(st["nanrow"].max().item()) if nray else nt
+        brk = mx if mx < nt else None
+        return RunResult(cnt[:, 0], cnt[:, 1], st["nanrow"], False, brk, n_live)
+
+
+def ctypes_ref(p):
+    import ctypes
+    return ctypes.byref(p)
+
+
+def kat_rk45(kind, y0, t_eval, rtol, atol, min_step, device="cuda"):
+    """Stepper KAT on the GPU: ``y0[nvar, ncol]`` -> ``ys[nt, nvar, ncol]``."""
+    H.require_gpu()
+    y0 = torch.as_tensor(y0, dtype=F64, device=device).contiguous()
+    te = torch.as_tensor(t_eval, dtype=F64, device=device).contiguous()
+    nv, ncol = y0.shape
+    out = torch.empty((ncol, len(t_eval), nv), dtype=F64, device=device)
+    H.check(H.load().rwrt_kat_rk45(int(kind), ncol, H.dptr(y0), len(t_eval), H.dptr(te),
+                                   float(max(rtol, 100 * np.finfo(np.float64).eps)), float(atol),
+                                   float(min_step), H.dptr(out), H.stream()))
+    return out.permute(1, 2, 0)

@@ -1,0 +1,43 @@
+"""The C-ABI library loads on the CPU-only build host and exports every declared symbol."""
+import ctypes
+import os
+import re
+
+import _hip as H
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    src = open(os.path.join(ROOT, "include", "rwrt.h")).read()
+    return sorted(set(re.findall(r"\b(rwrt_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_matches_binding():
+    assert header_symbols() == sorted(H.ABI_SYMBOLS)
+
+
+def test_library_exports_every_symbol():
+    lib = H.load()
+    for name in header_symbols():
+        assert hasattr(lib, name), name
+    assert "gfx950" in H.version()
+
+
+def test_struct_layouts():
+    # rwrt_grid: 2 x int32 + 4 x double; rwrt_params: 4 x double + 2 x int32
+    assert ctypes.sizeof(H.Grid) == 40
+    assert ctypes.sizeof(H.Params) == 40
+
+
+def test_argument_errors_are_reported_without_a_gpu():
+    """Argument validation happens before any HIP call: NULL grid -> RWRT_ERR_ARG."""
+    lib = H.load()
+    st = lib.rwrt_rhs(None, None, 0, None, None, None)
+    assert st == H.RWRT_ERR_ARG
+    assert b"grid" in lib.rwrt_last_error()
+    g = H.Grid(145, 73, 0.0, 0.04363323, -1.5707964, 0.04363323)
+    p = H.Params(1e-6, 1e-6, 7.2, 0.2, 1081, 0)
+    st = lib.rwrt_rk45_run(ctypes.byref(g), 16, 10, ctypes.byref(p), None, 0, 5, None, None,
+                           None, None, None, None, None)
+    assert st == H.RWRT_ERR_ARG
