@@ -134,6 +134,14 @@ rwrt_status rwrt_kat_rk45(int32_t kind, int64_t ncol, const double* d_y0,
                           double atol, double min_step, double* d_out,
                           void* stream);
 
+/* Device math self-test: d_out[i] = f(d_x[i], d_y[i]) with the exact device
+ * routines the kernels use.  kind: 0 sin(x), 1 cos(x), 2 tan(x), 3 pow(x, y),
+ * 4 atan2(x, y), 5 Python x % y (fmod-based), 6 sqrt(x), 7 x / y, 8 floor(x).
+ * Lets the tests prove which operations are bit-exact on the GPU (IEEE
+ * division, sqrt, fmod) and measure the last-bit agreement of the rest. */
+rwrt_status rwrt_selftest_math(int32_t kind, int64_t n, const double* d_x,
+                               const double* d_y, double* d_out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -666,6 +666,26 @@ __global__ void __launch_bounds__(256) rk45_run_kernel(RunArgs a) {
   }
 }
 
+__global__ void math_kernel(int kind, int64_t n, const double* __restrict__ x,
+                            const double* __restrict__ y, double* __restrict__ out) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double a = x[i], b = y ? y[i] : 0.0;
+  double r;
+  switch (kind) {
+    case 0: r = sin(a); break;
+    case 1: r = cos(a); break;
+    case 2: r = tan(a); break;
+    case 3: r = pow(a, b); break;
+    case 4: r = atan2(a, b); break;
+    case 5: r = py_mod(a, b); break;
+    case 6: r = sqrt(a); break;
+    case 7: r = a / b; break;
+    default: r = floor(a); break;
+  }
+  out[i] = r;
+}
+
 // rk45_simple_current (rkf45.py:672-724) over ncol columns, one lane each.
 template <class P>
 __global__ void kat_kernel(int64_t ncol, const double* __restrict__ y0, int32_t nt,
@@ -865,6 +885,16 @@ rwrt_status rwrt_kat_rk45(int32_t kind, int64_t ncol, const double* d_y0, int32_
     default: return fail(RWRT_ERR_ARG, "unknown KAT kind%s");
   }
   return check_launch("kat_kernel");
+}
+
+rwrt_status rwrt_selftest_math(int32_t kind, int64_t n, const double* d_x, const double* d_y,
+                               double* d_out, void* stream) {
+  if (n < 0 || kind < 0 || kind > 8 || (n > 0 && (!d_x || !d_out)))
+    return fail(RWRT_ERR_ARG, "bad selftest arguments%s");
+  if (n == 0) return RWRT_OK;
+  hipLaunchKernelGGL(math_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, kind,
+                     n, d_x, d_y, d_out);
+  return check_launch("math_kernel");
 }
 
 }  // extern "C"

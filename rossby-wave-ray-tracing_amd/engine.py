@@ -205,3 +205,18 @@ def kat_rk45(kind, y0, t_eval, rtol, atol, min_step, device="cuda"):
                                    float(max(rtol, 100 * np.finfo(np.float64).eps)), float(atol),
                                    float(min_step), H.dptr(out), H.stream()))
     return out.permute(1, 2, 0)
+
+
+MATH_KINDS = {"sin": 0, "cos": 1, "tan": 2, "pow": 3, "atan2": 4, "mod": 5, "sqrt": 6,
+              "div": 7, "floor": 8}
+
+
+def selftest_math(name, x, y=None, device="cuda"):
+    """Evaluate one device math routine element-wise (``rwrt_selftest_math``)."""
+    H.require_gpu()
+    x = torch.as_tensor(np.asarray(x, np.float64), device=device).contiguous()
+    yt = None if y is None else torch.as_tensor(np.asarray(y, np.float64), device=device).contiguous()
+    out = torch.empty_like(x)
+    H.check(H.load().rwrt_selftest_math(MATH_KINDS[name], x.numel(), H.dptr(x), H.dptr(yt),
+                                        H.dptr(out), H.stream()))
+    return out.cpu().numpy()

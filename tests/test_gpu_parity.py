@@ -161,26 +161,45 @@ def dpos(h_gpu, ref7, row):
     return np.max(np.abs(a[ok] - b[ok]), axis=1), ok
 
 
+def noise_floor(kind):
+    """The reference's own spread under 1-ulp RHS perturbations (tools/noise_floor.py)."""
+    import json
+    import os
+    from conftest import GOLDEN
+    return json.load(open(os.path.join(GOLDEN, f"noise_floor_C2_{kind}.json")))
+
+
 @pytest.mark.parametrize("kind", KINDS)
 def test_t2_c2_trajectories(kind):
+    """C2 (3 072 slots) against the reference's rows at 2 h, 1 d and 10 d.
+
+    Tolerances (per horizon, live rays): 2 h -- every ray within 1e-6 rad (the
+    north-star tolerance) and the same alive set; 1 d and 10 d -- the quantiles
+    of max(|dlon|, |dlat|) within 3x the reference's own 1-ulp noise floor
+    (tests/golden/noise_floor_C2_<kind>.json): beyond ~1 day no implementation
+    that is not bit-identical to NumPy's libm/SVML can do better.
+    """
     g = golden(f"traj_C2_{kind}.npz")
+    floor = noise_floor(kind)
     hist, res = run_c2(kind, int(g["nt"]))
     rows = list(g["rows"])
     ref = g["hist"]                          # (7, len(rows), nray)
-    # 2 h (row 1): every ray within 1e-6 rad, same alive set
-    d, ok = dpos(hist, ref[:, rows.index(1)], 1)
+    live = ~np.isnan(golden(f"init_C2_{kind}.npz")["rows"][3].reshape(-1))
+    # 2 h (row 1)
     assert np.array_equal(np.isnan(hist[:, 1, 0]), np.isnan(ref[0, rows.index(1)]))
+    d, ok = dpos(hist[live], ref[:, rows.index(1)][:, live], 1)
     assert d.max() <= 1e-6, d.max()
-    # 1 day (row 12): p99 within 1e-6 rad, max under the 1-ulp noise floor
-    d, ok = dpos(hist, ref[:, rows.index(12)], 12)
-    assert np.percentile(d, 99) <= 1e-6, np.percentile(d, 99)
-    assert d.max() <= 1.2e-5 * 10, d.max()
-    # 10 days (row 120): T3 -- alive set nearly identical, median |dpos| small
-    a_gpu = ~np.isnan(hist[:, 120, 0])
-    a_ref = ~np.isnan(ref[0, rows.index(120)])
-    assert abs(int(a_gpu.sum()) - int(a_ref.sum())) <= max(3, int(0.01 * a_ref.sum()))
-    d, ok = dpos(hist, ref[:, rows.index(120)], 120)
-    assert np.median(d) < 1e-4, np.median(d)
+    for row, key in [(12, "1d"), (120, "10d")]:
+        d, ok = dpos(hist[live], ref[:, rows.index(row)][:, live], row)
+        f = floor[key]
+        assert np.median(d) <= max(3 * f["p50"], 1e-12), (key, np.median(d), f["p50"])
+        assert np.percentile(d, 99) <= 3 * f["p99"], (key, np.percentile(d, 99), f["p99"])
+        if key == "1d":
+            assert d.max() <= 3 * f["max"], (key, d.max(), f["max"])
+    # T3 at 10 d: the alive set matches to within 1% of the live rays
+    a_gpu = ~np.isnan(hist[live, 120, 0])
+    a_ref = ~np.isnan(ref[0, rows.index(120)][live])
+    assert np.sum(a_gpu != a_ref) <= max(3, int(0.01 * live.sum()))
     # accepted ray-steps: same definition as the reference (counted by wrapping _step_impl)
     n_gpu = res.nacc.cpu().numpy()
     assert abs(int(n_gpu.sum()) - int(g["nacc"].sum())) <= 0.01 * int(g["nacc"].sum())
@@ -252,3 +271,31 @@ def test_kat_stepper():
     lo = kat_rk45(2, g["lorenz_y0"], ts, 1e-3, 1e-6, 0.001).cpu().numpy()
     k = np.searchsorted(ts, 2.0)
     assert np.max(np.abs(lo[:k] - g["lorenz_ys"][:k])) < 1e-6
+
+
+# ------------------------------------------------------------ device math
+def test_device_math_exactness():
+    """IEEE division, sqrt, floor and the Python modulo are bit-exact on the GPU;
+    sin/cos/tan/pow/atan2 agree with NumPy in the last bit for most inputs
+    (the residual is what bounds trajectory parity; rates recorded in DESIGN.md)."""
+    from engine import selftest_math
+    rng = np.random.default_rng(7)
+    n = 1 << 20
+    a = rng.uniform(-1e3, 1e3, n) * 10 ** rng.uniform(-6, 2, n)
+    b = rng.uniform(0.1, 10, n) * rng.choice([-1, 1], n)
+    assert np.array_equal(selftest_math("div", a, b), a / b)
+    pos = np.abs(a)
+    assert np.array_equal(selftest_math("sqrt", pos), np.sqrt(pos))
+    assert np.array_equal(selftest_math("floor", a), np.floor(a))
+    lon = np.concatenate([rng.uniform(-60, 80, n), [-0.0, 0.0, -1e-300, 2 * np.pi, -2 * np.pi]])
+    assert np.array_equal(selftest_math("mod", lon, np.full(lon.shape, 2 * np.pi)),
+                          lon % (2 * np.pi))
+    lat = rng.uniform(-1.5707963, 1.5707963, n)
+    rates = {}
+    for name in ("sin", "cos", "tan"):
+        rates[name] = float(np.mean(selftest_math(name, lat) != getattr(np, name)(lat)))
+    en = 10 ** rng.uniform(-4, 1, n)
+    rates["pow"] = float(np.mean(selftest_math("pow", en, np.full(n, -0.2)) != en ** -0.2))
+    print("device/NumPy last-bit mismatch rates:", rates)
+    assert rates["sin"] < 0.05 and rates["cos"] < 0.05 and rates["tan"] < 0.1
+    assert rates["pow"] < 0.2
