@@ -145,20 +145,28 @@ class RayEngine:
             H.stream()))
 
     def integrate(self, y0, nt, tstep, rtol=1e-6, atol=1e-6, msf=1e-3, cut_off=0.1,
-                  ttotal=None, chunk=None, sink=None, out=None, cut_rad=None, events=None):
+                  ttotal=None, chunk=None, sink=None, out=None, cut_rad=None, events=None,
+                  group=None):
         """The whole ray loop for ``y0[5, nray]``; rows 1..nt-1 go to ``sink``.
 
         ``sink(i0, i1, rows)`` receives each time chunk as a device tensor
         ``rows[nray, i1-i0, 8]`` (lon lat k l amp ug vg nacc) before the next
         chunk overwrites it.  ``events`` (a list) collects a pair of timing
-        events around every ray-loop launch.  Returns a ``RunResult``.
+        events around every ray-loop launch.  With a process ``group`` (rays
+        sharded over ranks, shard.py) the two global outcomes -- solver
+        failure and the all-NaN early exit -- are decided over every rank, so a
+        sharded run equals the single-GPU run.  Returns a ``RunResult``.
         """
         p = self.params(nt, tstep, rtol, atol, msf, cut_off, cut_rad)
         y0 = torch.as_tensor(y0, dtype=F64, device=self.device).contiguous()
         nray = y0.shape[1]
         tb = torch.as_tensor(t_eval_of(nt, tstep, ttotal), dtype=F64, device=self.device)
         st = self.init(y0, p)
-        summary = st["summary"].cpu()
+        summary = st["summary"]
+        if group is not None:
+            from shard import reduce_summary
+            summary = reduce_summary(summary, group)
+        summary = summary.cpu()
         n_live, n_finite = int(summary[0]), int(summary[1])
         cnt = st["count"]
         if n_live > 0 and n_finite == 0:
@@ -184,7 +192,10 @@ class RayEngine:
                 self.run(st, p, tb, i0, i1, view, order)
             if sink is not None:
                 sink(i0, i1, view)
-        mx = int(st["nanrow"].max().item()) if nray else nt
+        mx = int(st["nanrow"].max().item()) if nray else 0
+        if group is not None:
+            from shard import reduce_max
+            mx = reduce_max(mx, group)
         brk = mx if mx < nt else None
         return RunResult(cnt[:, 0], cnt[:, 1], st["nanrow"], False, brk, n_live)
 

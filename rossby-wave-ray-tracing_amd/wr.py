@@ -130,17 +130,35 @@ class WR:
         self.ray_initial_numpy(root_method=root_method)
 
     # ---------------------------------------------------------- ray loop
-    def core_ray_run_hip_rk45(self):
-        """The RK45 ray loop on the GPU (replaces wr.py:767-887)."""
+    def core_ray_run_hip_rk45(self, group=None):
+        """The RK45 ray loop on the GPU (replaces wr.py:767-887).
+
+        With a torch.distributed ``group`` of one process per GPU, the rays are
+        sharded over the ranks (shard.py): rank 0's basic state is broadcast,
+        every rank integrates its shard, and rank 0 gathers every output row
+        into its history arrays (the other ranks' arrays keep only row 0).
+        """
         import torch
+        import shard
+        rank, world = shard.world_info(group) if group is not None else (0, 1)
+        if world > 1:
+            self.bs.fields = shard.broadcast_array(self.bs.fields, 0, group)
+            self.bs._engine = None
         eng = self.bs.engine()
         nray = 3 * self.nsource * self.nzwn
         y0 = np.array([self.rlon[0], self.rlat[0], self.rzwn[0], self.rmwn[0],
                        self.ramp[0]], dtype=self.all_dtype).reshape(5, nray)
+        idx = np.arange(nray)
+        if world > 1:
+            idx = shard.shard_indices(~np.isnan(y0.mean(axis=0)), rank, world)
         rows_shape = (3, self.nsource, self.nzwn)
         hist = (self.rlon, self.rlat, self.rzwn, self.rmwn, self.ramp, self.rug, self.rvg)
 
         def sink(i0, i1, rows):
+            if world > 1:
+                rows = shard.gather_rows(rows, idx, nray, 0, group)
+                if rows is None:
+                    return
             host = rows[:, :, :7].permute(2, 1, 0).contiguous().cpu().numpy()
             for v in range(7):
                 hist[v][i0:i1] = host[v].reshape((i1 - i0,) + rows_shape)
@@ -148,25 +166,30 @@ class WR:
                 progress_bar(i1 - 1, self.nt)
 
         chunk = self.chunk_rows or _default_chunk(nray, self.nt)
-        res = eng.integrate(torch.as_tensor(y0), self.nt, float(self.tstep[0]), self.rtol,
-                            self.atol, self.MinStepFactor, ttotal=self.ttotal, chunk=chunk,
-                            sink=sink, cut_rad=float(self.cut_off[0]))
+        res = eng.integrate(torch.as_tensor(y0[:, idx]), self.nt, float(self.tstep[0]),
+                            self.rtol, self.atol, self.MinStepFactor, ttotal=self.ttotal,
+                            chunk=chunk, sink=sink, cut_rad=float(self.cut_off[0]),
+                            group=group if world > 1 else None)
         if res.break_row is not None:
             for h in hist:
                 h[res.break_row:] = np.nan     # rows never stored (wr.py:853-855, 886-887)
         self.last_run = res
         return res
 
-    def core_ray_run(self, mode="hip_rk45"):
+    def core_ray_run(self, mode="hip_rk45", group=None):
         if mode not in SUPPORTED:
             raise NotImplementedError(
                 f"ray loop {mode!r} is not provided by this framework; use "
                 f"ray_run(mode='hip', inte_method='rk45') (the MI355X RK45 ray loop)")
-        return self.core_ray_run_hip_rk45()
+        return self.core_ray_run_hip_rk45(group=group)
 
     def ray_run(self, mode="hip", inte_method="rk45", root_method="numpy", debug=False,
-                debug_file=None):
-        """Initialise and integrate all rays (wr.py:897-911)."""
+                debug_file=None, group=None):
+        """Initialise and integrate all rays (wr.py:897-911).
+
+        ``group``: optional torch.distributed process group (one rank per GPU)
+        to shard the rays across GPUs; results land on rank 0.
+        """
         key = mode + "_rk45" if inte_method == "rk45" else mode
         if key not in SUPPORTED:
             self.core_ray_run(key)     # raises before any work
@@ -176,7 +199,7 @@ class WR:
                 self.load_init_from_precal_nc(debug_file)
             except Exception:
                 pass
-        return self.core_ray_run(key)
+        return self.core_ray_run(key, group=group)
 
     def load_init_from_precal_nc(self, ncfile):
         """Seed row 0 from a previously written ray file (wr.py:398-415)."""

@@ -5,6 +5,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "rossby-wave-ray-tracing_amd")
+os.environ.setdefault("PYTHONPATH", os.pathsep.join([PKG, os.path.join(ROOT, "oracle"), ROOT]))
 for p in (PKG, os.path.join(ROOT, "oracle"), ROOT):
     if p not in sys.path:
         sys.path.insert(0, p)

@@ -1,0 +1,84 @@
+"""Multi-rank plumbing of shard.py on the CPU: world size 2 over gloo (127.0.0.1).
+
+The GPU kernel cannot run here; the per-ray integration is replaced by a
+deterministic per-ray function so that the sharded pipeline (split, broadcast,
+per-rank work, global reductions, gather) can be checked against the
+unsharded result exactly.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def fake_integrate(y0):
+    """Stands in for RayEngine.integrate: per-ray rows (nray, 3, 8)."""
+    t = torch.as_tensor(y0).T.contiguous()
+    rows = torch.stack([t.sum(1), t.prod(1), t[:, 0] * 2, t[:, 1] - 1,
+                        t[:, 2], t[:, 3], t[:, 4], torch.zeros(t.shape[0], dtype=t.dtype)], 1)
+    return torch.stack([rows, rows * 2, rows * 3], 1)
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import shard
+        rng = np.random.default_rng(0)
+        nray = 101
+        y0 = rng.standard_normal((5, nray)) if rank == 0 else None
+        y0 = shard.broadcast_array(y0 if rank == 0 else np.zeros(1), 0)
+        y0[:, ::3] = np.nan                                 # dead slots
+        live = ~np.isnan(y0.mean(axis=0))
+        idx = shard.shard_indices(live, rank, world)
+        local = fake_integrate(y0[:, idx])
+        full = shard.gather_rows(local, idx, nray, 0)
+        summ = shard.reduce_summary(torch.tensor([int(live[idx].sum()), rank], dtype=torch.int64))
+        mx = shard.reduce_max(10 + rank)
+        if rank == 0:
+            q.put(("ok", full.numpy(), fake_integrate(y0).numpy(), summ.tolist(), mx,
+                   int(live.sum())))
+    except Exception as e:  # pragma: no cover
+        q.put(("err", repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_shard_indices_partition_and_balance():
+    import shard
+    live = np.random.default_rng(1).random(1000) < 0.3
+    parts = [shard.shard_indices(live, r, 4) for r in range(4)]
+    allidx = np.sort(np.concatenate(parts))
+    assert np.array_equal(allidx, np.arange(1000))
+    nl = [int(live[p].sum()) for p in parts]
+    assert max(nl) - min(nl) <= 1
+
+
+def test_world2_gloo_pipeline_equals_unsharded():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+    assert res[0] == "ok", res
+    _, full, ref, summ, mx, nlive = res
+    assert np.array_equal(full, ref, equal_nan=True)
+    assert summ == [nlive, 1]
+    assert mx == 11
