@@ -89,7 +89,17 @@ def main():
     ap.add_argument("--cpu-days", type=float, default=4.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--periods", type=int, default=5, help="C3 periods in the batch (1-5)")
+    ap.add_argument("--order", default="priority", choices=["priority", "cost", "live"],
+                    help="work-queue order: heaviest rays to high-priority waves (priority), "
+                         "longest-first (cost), or live-first")
+    ap.add_argument("--first-chunk", type=int, default=6,
+                    help="rows of the short first launch that measures per-ray cost")
+    ap.add_argument("--lib", default=None, help="alternative librwrt build (A/B timing)")
+    ap.add_argument("--replicate", type=int, default=1,
+                    help="diagnostic: repeat the ray batch k times (more rays per lane)")
     args = ap.parse_args()
+    if args.lib:
+        os.environ["RWRT_LIB"] = os.path.abspath(args.lib)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -107,6 +117,8 @@ def main():
     y0 = c3_initial_state(bs, lon_offset_deg=rank * 2.0 / max(world, 1),
                           periods=S.C3_PERIODS_DAYS[: args.periods])
     t_init = time.perf_counter() - t_init
+    if args.replicate > 1:
+        y0 = np.concatenate([y0] * args.replicate, axis=1)
     nslot = y0.shape[1]
     n_live = int(np.sum(~np.isnan(y0.mean(axis=0))))
     eng = RayEngine.from_bs(bs, device=dev)
@@ -117,7 +129,8 @@ def main():
 
     def one_step(events=None):
         return eng.integrate(y0_d, nt, 7200.0, ttotal=(nt - 1) * 7200.0, chunk=chunk, out=out,
-                             events=events)
+                             events=events, order_policy=args.order,
+                             first_chunk=args.first_chunk)
 
     for _ in range(args.warmup):
         one_step()
@@ -165,6 +178,8 @@ def main():
             "ray_steps_per_step": steps_done / args.steps,
             "rejected_per_accepted": rej / max(r.ray_steps, 1),
             "host_init_s": t_init,
+            "queue_order": args.order,
+            "library": os.path.basename(os.environ.get("RWRT_LIB", "librwrt.so")),
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK, "traffic": None,
                          "kernel": "rk45_run_kernel", "avg_launch_ms": 1e3 * avg_launch_s,

@@ -111,17 +111,19 @@ rwrt_status rwrt_rk45_init(const rwrt_grid* g, const double* d_packed,
  * it_begin <= i < it_end (1 <= it_begin < it_end <= nt): every ray is stepped
  * to d_tbound[i] (t_eval, wr.py:798-801) with the reference's step control
  * (rkf45.py:222-253,375-514), then masked (wr.py:838-850) and its group
- * velocity recomputed (wr.py:856-865).  Rays are taken from a device work
- * queue in the order d_order[nray] (NULL = 0..nray-1).  Output row r of ray j
- * is d_out[(j*(it_end-it_begin) + r)*8 + {lon,lat,k,l,amp,ug,vg,nacc}].
+ * velocity recomputed (wr.py:856-865).  Rays are taken from device work
+ * queues in the order d_order[nray] (NULL = 0..nray-1): the first n_heavy
+ * entries are served first by one high-priority wave per SIMD (pass the
+ * rays expected to be slowest there; 0 = a single queue).  Output row r of
+ * ray j is d_out[(j*(it_end-it_begin) + r)*8 + {lon,lat,k,l,amp,ug,vg,nacc}].
  * d_state / d_count / d_nanrow carry the per-ray solver state across calls
- * (time chunking).  d_work: >= 1 int32 of scratch (the queue head), reset by
- * this call on `stream`. */
+ * (time chunking).  d_work: >= 2 int32 of scratch (queue heads), reset by
+ * this call on `stream`.  Results do not depend on the order or n_heavy. */
 rwrt_status rwrt_rk45_run(const rwrt_grid* g, const double* d_packed,
                           int64_t nray, const rwrt_params* p,
                           const double* d_tbound, int32_t it_begin,
                           int32_t it_end, const int64_t* d_order,
-                          double* d_state, int64_t* d_count,
+                          int64_t n_heavy, double* d_state, int64_t* d_count,
                           int32_t* d_nanrow, double* d_out, int32_t* d_work,
                           void* stream);
 
@@ -136,7 +138,9 @@ rwrt_status rwrt_kat_rk45(int32_t kind, int64_t ncol, const double* d_y0,
 
 /* Device math self-test: d_out[i] = f(d_x[i], d_y[i]) with the exact device
  * routines the kernels use.  kind: 0 sin(x), 1 cos(x), 2 tan(x), 3 pow(x, y),
- * 4 atan2(x, y), 5 Python x % y (fmod-based), 6 sqrt(x), 7 x / y, 8 floor(x).
+ * 4 atan2(x, y), 5 Python x % y (fmod-based), 6 sqrt(x), 7 x / y, 8 floor(x),
+ * 9/10 sin/cos through sincos(x), 11 x / 6.3712e6 (the kernels' exact division
+ * by the earth radius), 12 fmod(x, y) for y > 0 (the kernels' exact fmod).
  * Lets the tests prove which operations are bit-exact on the GPU (IEEE
  * division, sqrt, fmod) and measure the last-bit agreement of the rest. */
 rwrt_status rwrt_selftest_math(int32_t kind, int64_t n, const double* d_x,

@@ -65,7 +65,7 @@ def load():
         "rwrt_rhs": [G, _P, _I64, _P, _P, _P],
         "rwrt_dp54_attempt": [G, _P, _I64, _P, _P, _P, _D, _D, _P, _P, _P, _P],
         "rwrt_rk45_init": [G, _P, _I64, _P, Pr, _P, _P, _P, _P, _P, _P],
-        "rwrt_rk45_run": [G, _P, _I64, Pr, _P, _I32, _I32, _P, _P, _P, _P, _P, _P, _P],
+        "rwrt_rk45_run": [G, _P, _I64, Pr, _P, _I32, _I32, _P, _I64, _P, _P, _P, _P, _P, _P],
         "rwrt_kat_rk45": [_I32, _I64, _P, _I32, _P, _D, _D, _D, _P, _P],
         "rwrt_selftest_math": [_I32, _I64, _P, _P, _P, _P],
     }

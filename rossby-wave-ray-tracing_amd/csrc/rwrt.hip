@@ -29,6 +29,20 @@ constexpr double kPi = 3.14159265358979323846;
 constexpr double kHalfPi = 0.5 * kPi;  // "0.5 * pi"  wr.py:508, bs.py:787
 constexpr double kTwoPi = 2.0 * kPi;   // "2 * pi"    bs.py:519, interpolation.py:80
 constexpr double kREarth = 6.3712e6;
+constexpr double kRInv = 1.0 / 6.3712e6;   // RN(1 / R)
+
+// x / R correctly rounded without the division sequence (Markstein): q0 is
+// within an ulp of x/R, the FMA remainder r = x - q0 R is exact, and one more
+// FMA rounds q0 + r/R correctly.  Zero, tiny, huge and non-finite x take the
+// IEEE division (signed zeros, gradual underflow).  Verified bit-exact against
+// IEEE division on the device (tests/test_gpu_parity.py).
+__device__ __forceinline__ double div_rearth(double x) {
+  const double ax = fabs(x);
+  if (!(ax > 0x1p-900 && ax < 0x1p900)) return x / kREarth;
+  const double q0 = x * kRInv;
+  const double r = fma(-q0, kREarth, x);
+  return fma(r, kRInv, q0);
+}
 constexpr double kNaN = __builtin_nan("");
 
 // rkf45.py:604-615 (Dormand-Prince 5(4)); C++ constant division is IEEE
@@ -63,10 +77,33 @@ __device__ __forceinline__ double np_max(double a, double b) {
 __device__ __forceinline__ double np_min(double a, double b) {
   return (a <= b || a != a) ? a : b;
 }
+// fmod(a, b) for b > 0, exact (fmod is always exactly representable): for
+// |a| < 2^40 the integer quotient n = trunc(|a|/b) is off by at most one; the
+// remainder |a| - n b is a multiple of ulp(b) below b, so one FMA computes it
+// exactly, and a wrong n shows up as a remainder outside [0, b) (a sign test,
+// which rounding cannot flip).  A third of the library routine's cost.
+__device__ __forceinline__ double fmod_pos(double a, double b) {
+  const double x = fabs(a);
+  if (!(x < 0x1p40)) return fmod(a, b);      // NaN, inf, huge: library routine
+  double r = x;
+  if (x >= b) {
+    double n = trunc(x / b);
+    r = fma(-n, b, x);
+    if (r < 0.0) {
+      n -= 1.0;
+      r = fma(-n, b, x);
+    } else if (r >= b) {
+      n += 1.0;
+      r = fma(-n, b, x);
+    }
+  }
+  return copysign(r, a);
+}
+
 // Python/NumPy floor modulo for float64 (npy_remainder): fmod, then move a
 // remainder whose sign differs from b into [0, b); exact zero gets b's sign.
 __device__ __forceinline__ double py_mod(double a, double b) {
-  double m = fmod(a, b);
+  double m = fmod_pos(a, b);
   if (m != 0.0) {
     if ((b < 0.0) != (m < 0.0)) m += b;
   } else {
@@ -92,6 +129,10 @@ constexpr int kNF = RWRT_NFIELD_PACK;
 // slot -> index in the reference 18-field stack (bs.py:349-368); qyx (10) and
 // the six third derivatives are never read on the hot path.
 __constant__ int kRefIndex[11] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 11};
+
+#ifndef RWRT_INTERP_GROUP
+#define RWRT_INTERP_GROUP 6   // records (of 2 fields) per load group, divides 6
+#endif
 
 struct Field {
   const double* __restrict__ P;
@@ -147,11 +188,17 @@ __device__ __forceinline__ void interp11(const Field& F, double lon, double lat,
   const double2* pb = reinterpret_cast<const double2*>(k.b);
   const double2* pc = reinterpret_cast<const double2*>(k.c);
   const double2* pd = reinterpret_cast<const double2*>(k.d);
+  // Three groups of 2 records x 4 corners: bounds the registers held by
+  // in-flight loads (the lookup is L2-resident; occupancy hides the latency).
 #pragma unroll
-  for (int q = 0; q < 6; ++q) {
-    const double2 va = pa[q], vb = pb[q], vc = pc[q], vd = pd[q];
-    g[2 * q] = blend(k, va.x, vb.x, vc.x, vd.x);
-    if (2 * q + 1 < 11) g[2 * q + 1] = blend(k, va.y, vb.y, vc.y, vd.y);
+  for (int q0 = 0; q0 < 6; q0 += RWRT_INTERP_GROUP) {
+#pragma unroll
+    for (int q = q0; q < q0 + RWRT_INTERP_GROUP; ++q) {
+      const double2 va = pa[q], vb = pb[q], vc = pc[q], vd = pd[q];
+      g[2 * q] = blend(k, va.x, vb.x, vc.x, vd.x);
+      if (2 * q + 1 < 11) g[2 * q + 1] = blend(k, va.y, vb.y, vc.y, vd.y);
+    }
+    if (q0 + RWRT_INTERP_GROUP < 6) __builtin_amdgcn_sched_barrier(0);
   }
 }
 
@@ -234,7 +281,9 @@ __device__ __forceinline__ void ray_rhs(const Field& F, const double* y, double*
   }
   double g[11];
   interp11(F, py_mod(lon, kTwoPi), lat, g);
-  const double c = cos(lat), s = sin(lat), tn = tan(lat);
+  double s, c;
+  sincos(lat, &s, &c);              // one argument reduction for both (== sin(), cos())
+  const double tn = tan(lat);
   const Merc M = merc_factors(lat, c, s);
   double o[12];
   mercator12(g, M, tn, o);
@@ -253,11 +302,11 @@ __device__ __forceinline__ void ray_rhs(const Field& F, const double* y, double*
   const double damp2 = (2.0 * (kap * (fmqxx - fmqyy) + (kap2 - 1.0) * fmqxy)) / (kk * kap1);
   const double damp3 = (-2.0 * s) * fmv;
   const double damp = (damp1 + damp2) + damp3;
-  dy[0] = ug / kREarth;
-  dy[1] = (vg * c) / kREarth;
-  dy[2] = dzwn / kREarth;
-  dy[3] = dmwn / kREarth;
-  dy[4] = (damp * amp) / kREarth;
+  dy[0] = div_rearth(ug);
+  dy[1] = div_rearth(vg * c);
+  dy[2] = div_rearth(dzwn);
+  dy[3] = div_rearth(dmwn);
+  dy[4] = div_rearth(damp * amp);
 }
 
 // group velocity at a stored position (wr.py:856-865): no |l| mask here
@@ -319,65 +368,128 @@ struct KatLorenz {
 // ---------------------------------------------------------------------------
 // Dormand-Prince 5(4) attempt, rk_step (rkf45.py:259-321) + error norm
 // ---------------------------------------------------------------------------
-// np.einsum('snf,s->nf', K[:S], w) in NumPy's order: sequential in s for more
-// than one variable; for one variable einsum's 2-lane SIMD dot product sums the
-// even and the odd terms separately (oracle/rwrt_oracle.py wsum).
-template <int NV, int S>
-__device__ __forceinline__ double wsum(const double (&K)[7][NV], const double* w, int v) {
+// Stage weights: row s = 1..5 is A[s][0..4] (stage inputs), row 6 is B[0..5]
+// (y_new); the time offset of stage 6 is c = 1 (K6 = fun(t + h, y_new)).
+__constant__ double kW[7][6] = {
+    {0, 0, 0, 0, 0, 0},
+    {kA[1][0], 0, 0, 0, 0, 0},
+    {kA[2][0], kA[2][1], 0, 0, 0, 0},
+    {kA[3][0], kA[3][1], kA[3][2], 0, 0, 0},
+    {kA[4][0], kA[4][1], kA[4][2], kA[4][3], 0, 0},
+    {kA[5][0], kA[5][1], kA[5][2], kA[5][3], kA[5][4], 0},
+    {kB[0], kB[1], kB[2], kB[3], kB[4], kB[5]}};
+__constant__ double kCs[7] = {0.0, kC[1], kC[2], kC[3], kC[4], kC[5], 1.0};
+
+// Storage of the stages K0..K5 of one attempt, per lane: in registers, or in a
+// per-thread slice of LDS (frees 60 VGPRs of the ray kernel for occupancy).
+template <int NV>
+struct KRegs {
+  double k[6][NV];
+  __device__ __forceinline__ double get(int j, int v) const { return k[j][v]; }
+  __device__ __forceinline__ void put(int j, int v, double x) { k[j][v] = x; }
+  // stage index s is wave-uniform; select the register row statically
+  __device__ __forceinline__ void put_stage(int s, const double* r) {
+#pragma unroll
+    for (int j = 0; j < 6; ++j)
+      if (j == s) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v) k[j][v] = r[v];
+      }
+  }
+};
+
+template <int NV>
+struct KShared {
+  double* p;   // this lane's slice: element (j, v) at p[(j * NV + v) * stride]
+  int stride;  // threads per block
+  __device__ __forceinline__ double get(int j, int v) const { return p[(j * NV + v) * stride]; }
+  __device__ __forceinline__ void put(int j, int v, double x) { p[(j * NV + v) * stride] = x; }
+  __device__ __forceinline__ void put_stage(int s, const double* r) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) p[(s * NV + v) * stride] = r[v];
+  }
+};
+
+// np.einsum('snf,s->nf', K[:s], w) in NumPy's order, s <= 6 wave-uniform:
+// sequential in j for more than one variable; for one variable einsum's
+// 2-lane SIMD dot product sums even and odd terms separately
+// (oracle/rwrt_oracle.py wsum).
+template <int NV, class KS>
+__device__ __forceinline__ double wsum(const KS& K, const double* w, int s, int v) {
   if constexpr (NV == 1) {
     double even = 0.0, odd = 0.0;
 #pragma unroll
-    for (int j = 0; j < S; ++j) {
-      if (j % 2 == 0) even = even + K[j][v] * w[j];
-      else odd = odd + K[j][v] * w[j];
+    for (int j = 0; j < 6; ++j) {
+      if (j < s) {
+        if (j % 2 == 0) even = even + K.get(j, v) * w[j];
+        else odd = odd + K.get(j, v) * w[j];
+      }
     }
     return even + odd;
   } else {
     double acc = 0.0;
 #pragma unroll
-    for (int j = 0; j < S; ++j) acc = acc + K[j][v] * w[j];
+    for (int j = 0; j < 6; ++j)
+      if (j < s) acc = acc + K.get(j, v) * w[j];
     return acc;
   }
 }
 
-template <int S, int NV>
-__device__ __forceinline__ void stage_point(const double (&K)[7][NV], const double* y, double h,
-                                            double* ys) {
-#pragma unroll
-  for (int v = 0; v < NV; ++v) ys[v] = y[v] + wsum<NV, S>(K, kA[S], v) * h;
-}
-
-// Returns the error norm (NaN kept); fills y_new and K.
-template <class P>
-__device__ __forceinline__ double dp54_attempt(const P& fun, double t, const double* y,
+// One DP5(4) attempt: rk_step (rkf45.py:259-321) + _estimate_error_norm
+// (rkf45.py:368-373).  The six stage evaluations share ONE inlined copy of the
+// RHS (a wave-uniform stage loop), which keeps the kernel's code small and its
+// register file for occupancy.  Returns the error norm (NaN kept); fills y_new,
+// K6 and, if Kout is given, all seven stages.
+template <class P, class KS>
+__device__ __forceinline__ double dp54_attempt(const P& fun, KS& K, double t, const double* y,
                                                const double* f, double h, double rtol,
-                                               double atol, double (&K)[7][P::NV],
-                                               double* ynew) {
+                                               double atol, double* ynew, double* k6,
+                                               double* Kout = nullptr, int64_t kstride = 0) {
   constexpr int NV = P::NV;
-  double ys[NV];
 #pragma unroll
-  for (int v = 0; v < NV; ++v) K[0][v] = f[v];
-  stage_point<1>(K, y, h, ys);
-  fun(t + kC[1] * h, ys, K[1]);
-  stage_point<2>(K, y, h, ys);
-  fun(t + kC[2] * h, ys, K[2]);
-  stage_point<3>(K, y, h, ys);
-  fun(t + kC[3] * h, ys, K[3]);
-  stage_point<4>(K, y, h, ys);
-  fun(t + kC[4] * h, ys, K[4]);
-  stage_point<5>(K, y, h, ys);
-  fun(t + kC[5] * h, ys, K[5]);
+  for (int v = 0; v < NV; ++v) K.put(0, v, f[v]);
+  double ys[NV], r[NV];
+#pragma nounroll
+  for (int s = 1; s <= 6; ++s) {
 #pragma unroll
-  for (int v = 0; v < NV; ++v) ynew[v] = y[v] + h * wsum<NV, 6>(K, kB, v);
-  fun(t + h, ynew, K[6]);
-  // _estimate_error_norm: norm(h * (E . K) / scale), scale = atol + max(|y|,|y_new|) rtol
+    for (int v = 0; v < NV; ++v) ys[v] = y[v] + wsum<NV>(K, kW[s], s, v) * h;
+    fun(t + kCs[s] * h, ys, r);
+    if (s < 6) K.put_stage(s, r);
+  }
+  // after the loop: ys = y + h*(B . K[:6]) = y_new, r = K6
   double ss = 0.0;
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
-    const double e = h * wsum<NV, 7>(K, kE, v);
-    const double sc = atol + np_max(fabs(y[v]), fabs(ynew[v])) * rtol;
+    ynew[v] = ys[v];
+    k6[v] = r[v];
+    double es;
+    if constexpr (NV == 1) {
+      double even = 0.0, odd = 0.0;
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        if (j % 2 == 0) even = even + K.get(j, v) * kE[j];
+        else odd = odd + K.get(j, v) * kE[j];
+      }
+      even = even + r[v] * kE[6];
+      es = even + odd;
+    } else {
+      es = 0.0;
+#pragma unroll
+      for (int j = 0; j < 6; ++j) es = es + K.get(j, v) * kE[j];
+      es = es + r[v] * kE[6];
+    }
+    const double e = h * es;
+    const double sc = atol + np_max(fabs(y[v]), fabs(ys[v])) * rtol;
     const double x = e / sc;
     ss = (v == 0) ? x * x : ss + x * x;
+  }
+  if (Kout) {
+#pragma unroll
+    for (int j = 0; j < 6; ++j)
+#pragma unroll
+      for (int v = 0; v < NV; ++v) Kout[(j * NV + v) * kstride] = K.get(j, v);
+#pragma unroll
+    for (int v = 0; v < NV; ++v) Kout[(6 * NV + v) * kstride] = r[v];
   }
   return sqrt(ss) / RootN<NV>::v;
 }
@@ -423,24 +535,29 @@ __device__ __forceinline__ double initial_step(const P& fun, double t0, const do
 // One lane's solver: the per-column part of OdeSolver.step / _step_impl
 // (rkf45.py:222-253, 375-514).  iterate() runs at most ONE attempt and
 // reports whether the column reached t_bound.
-template <class P>
+template <class P, class KS>
 struct Lane {
   static constexpr int NV = P::NV;
+  KS K;
   double y[NV], f[NV];
   double t, habs, hs;
   bool in_step, rejected;
 
-  __device__ __forceinline__ bool iterate(const P& fun, double tb, double min_step, double rtol,
-                                          double atol, int64_t& nacc, int64_t& nrej) {
+  // Returns kStep (attempt made, interval not finished), kReached (t == t_bound)
+  // or kFrozen (NaN mean at step start: t := t_bound, y never changes again).
+  enum { kStep = 0, kReached = 1, kFrozen = 2 };
+
+  __device__ __forceinline__ int iterate(const P& fun, double tb, double min_step, double rtol,
+                                         double atol, int64_t& nacc, int64_t& nrej) {
     if (!in_step) {
       double sum = y[0];
 #pragma unroll
       for (int v = 1; v < NV; ++v) sum = sum + y[v];
       if (isnan(sum / (double)NV)) {  // NaN mean: frozen, t := t_bound (rkf45.py:400-403)
         t = tb;
-        return true;
+        return kFrozen;
       }
-      if (t == tb) return true;
+      if (t == tb) return kReached;
       if (!P::kAutonomous) fun(t, y, f);   // rkf45.py:378 (equal to K6 if autonomous)
       hs = np_max(habs, min_step);         // rkf45.py:383-387
       rejected = false;
@@ -451,8 +568,8 @@ struct Lane {
     if (tn - tb > 0.0) tn = tb;             // rkf45.py:429
     h = tn - t;
     const double ha = fabs(h);
-    double K[7][NV], yn[NV];
-    double en = dp54_attempt(fun, t, y, f, h, rtol, atol, K, yn);
+    double yn[NV], k6[NV];
+    double en = dp54_attempt(fun, K, t, y, f, h, rtol, atol, yn, k6);
     if (en != en) en = 0.0;                 // rkf45.py:446
     if (en < 1.0) {
       double fac = np_min(kMaxFactor, kSafety * pow(en, kErrExp));
@@ -463,16 +580,16 @@ struct Lane {
 #pragma unroll
       for (int v = 0; v < NV; ++v) {
         y[v] = yn[v];
-        f[v] = K[6][v];
+        f[v] = k6[v];
       }
       in_step = false;
       ++nacc;
-      return t - tb >= 0.0;                 // rkf45.py:250
+      return (t - tb >= 0.0) ? kReached : kStep;   // rkf45.py:250
     }
     hs = ha * np_max(kMinFactor, kSafety * pow(en, kErrExp));
     rejected = true;
     ++nrej;
-    return false;
+    return kStep;
   }
 };
 
@@ -524,19 +641,16 @@ __global__ void attempt_kernel(Field F, int64_t n, const double* __restrict__ y,
   const RayProblem P{F};
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
-    double yy[5], ff[5], K[7][5], yn[5];
+    double yy[5], ff[5], yn[5], k6[5];
 #pragma unroll
     for (int v = 0; v < 5; ++v) {
       yy[v] = y[v * n + i];
       ff[v] = f[v * n + i];
     }
-    err[i] = dp54_attempt(P, 0.0, yy, ff, h[i], rtol, atol, K, yn);
+    KRegs<5> K;
+    err[i] = dp54_attempt(P, K, 0.0, yy, ff, h[i], rtol, atol, yn, k6, Kout + i, n);
 #pragma unroll
     for (int v = 0; v < 5; ++v) ynew[v * n + i] = yn[v];
-#pragma unroll
-    for (int s = 0; s < 7; ++s)
-#pragma unroll
-      for (int v = 0; v < 5; ++v) Kout[(s * 5 + v) * n + i] = K[s][v];
   }
 }
 
@@ -593,23 +707,63 @@ struct RunArgs {
   int64_t* count;
   int32_t* nanrow;
   double* out;
-  int32_t* queue;
+  int32_t* queue;       // [0] heavy-queue head, [1] light-queue head
+  int64_t n_heavy;      // order[0, n_heavy) = heavy queue, the rest = light queue
+  int32_t heavy_blocks; // blocks [0, heavy_blocks) serve the heavy queue first
 };
 
 // WR.core_ray_run_rk45 (wr.py:767-887) for rows [it_begin, it_end): persistent
 // lanes, one ray each, refilled from the work queue.
-__global__ void __launch_bounds__(256) rk45_run_kernel(RunArgs a) {
+//
+// Load balance: the work per ray per chunk spans 15x the mean (C3); the
+// slowest rays set the makespan.  The host orders rays by the work they did in
+// the previous chunk and hands the heaviest ones to one high-priority wave per
+// SIMD (blocks [0, heavy_blocks), s_setprio 3): those rays' lanes get the
+// SIMD's issue slots first and the critical path runs at single-wave speed,
+// while the normal-priority waves fill every stall.
+#ifndef RWRT_WAVES_PER_SIMD
+#define RWRT_WAVES_PER_SIMD 1
+#endif
+#ifndef RWRT_K_IN_LDS
+#define RWRT_K_IN_LDS 1   // stages in LDS: frees 60 VGPRs (in registers they spill to scratch)
+#endif
+#if RWRT_K_IN_LDS
+using KStore = KShared<5>;
+#else
+using KStore = KRegs<5>;
+#endif
+__global__ void __launch_bounds__(256, RWRT_WAVES_PER_SIMD) rk45_run_kernel(RunArgs a) {
   const RayProblem P{a.F};
   const int64_t nrows = a.it_end - a.it_begin;
-  Lane<RayProblem> L;
+#if RWRT_K_IN_LDS
+  __shared__ double kbuf[6 * 5 * 256];
+  Lane<RayProblem, KStore> L;
+  L.K.p = kbuf + threadIdx.x;
+  L.K.stride = 256;
+#else
+  Lane<RayProblem, KStore> L;
+#endif
   int64_t ray = -1, nacc = 0, nrej = 0;
   int32_t it = 0, nanrow = 0;
   double prev_lon = 0.0, prev_lat = 0.0;
+  const bool heavy = (int)blockIdx.x < a.heavy_blocks;
+  bool heavy_left = heavy && a.n_heavy > 0;
+  if (heavy) __builtin_amdgcn_s_setprio(3);
   for (;;) {
     if (ray < 0) {
-      const int32_t w = atomicAdd(a.queue, 1);
-      if (w >= a.nray) break;
-      ray = a.order ? a.order[w] : (int64_t)w;
+      int64_t w = -1;
+      if (heavy_left) {
+        w = atomicAdd(&a.queue[0], 1);
+        if (w >= a.n_heavy) {
+          heavy_left = false;
+          w = -1;
+        }
+      }
+      if (w < 0) {
+        w = a.n_heavy + atomicAdd(&a.queue[1], 1);
+        if (w >= a.nray) break;
+      }
+      ray = a.order ? a.order[w] : w;
 #pragma unroll
       for (int v = 0; v < 5; ++v) {
         L.y[v] = a.state[v * a.nray + ray];
@@ -628,7 +782,8 @@ __global__ void __launch_bounds__(256) rk45_run_kernel(RunArgs a) {
       prev_lat = L.y[1];
     }
     const double tb = a.tbound[it];
-    if (!L.iterate(P, tb, a.min_step, a.rtol, a.atol, nacc, nrej)) continue;
+    const int st = L.iterate(P, tb, a.min_step, a.rtol, a.atol, nacc, nrej);
+    if (st == Lane<RayProblem, KStore>::kStep) continue;
 
     // ---- interval it reached: post-processing (wr.py:835-885) ----
     double* y = L.y;
@@ -642,15 +797,25 @@ __global__ void __launch_bounds__(256) rk45_run_kernel(RunArgs a) {
     }
     double ug, vg;
     ugvg_at(a.F, y[0], y[1], y[2], y[3], ug, vg);
-    double2* o = reinterpret_cast<double2*>(a.out + ((size_t)ray * nrows + (it - a.it_begin)) * RWRT_NOUT);
-    o[0] = make_double2(y[0], y[1]);
-    o[1] = make_double2(y[2], y[3]);
-    o[2] = make_double2(y[4], ug);
-    o[3] = make_double2(vg, (double)nacc);
+    const double2 r0 = make_double2(y[0], y[1]), r1 = make_double2(y[2], y[3]);
+    const double2 r2 = make_double2(y[4], ug), r3 = make_double2(vg, (double)nacc);
+    // A frozen ray never changes again (its mean stays NaN; re-applying the
+    // masks against itself is a no-op), so every remaining row of the chunk
+    // equals this one: write them all and release the lane.
+    const int last = (st == Lane<RayProblem, KStore>::kFrozen) ? a.it_end : it + 1;
+    for (int k = it; k < last; ++k) {
+      double2* o = reinterpret_cast<double2*>(a.out + ((size_t)ray * nrows + (k - a.it_begin)) * RWRT_NOUT);
+      o[0] = r0;
+      o[1] = r1;
+      o[2] = r2;
+      o[3] = r3;
+    }
+    if (nanrow == a.nt && isnan(y[0])) nanrow = it;  // wr.py:853-855 (host reduces)
     prev_lon = y[0];
     prev_lat = y[1];
-    if (nanrow == a.nt && isnan(y[0])) nanrow = it;  // wr.py:853-855 (host reduces)
-    if (++it == a.it_end) {
+    it = last;
+    if (st == Lane<RayProblem, KStore>::kFrozen) L.t = a.tbound[a.it_end - 1];
+    if (it == a.it_end) {
 #pragma unroll
       for (int v = 0; v < 5; ++v) {
         a.state[v * a.nray + ray] = y[v];
@@ -681,7 +846,11 @@ __global__ void math_kernel(int kind, int64_t n, const double* __restrict__ x,
     case 5: r = py_mod(a, b); break;
     case 6: r = sqrt(a); break;
     case 7: r = a / b; break;
-    default: r = floor(a); break;
+    case 8: r = floor(a); break;
+    case 9: { double sn, cs; sincos(a, &sn, &cs); r = sn; } break;
+    case 10: { double sn, cs; sincos(a, &sn, &cs); r = cs; } break;
+    case 11: r = div_rearth(a); break;
+    default: r = fmod_pos(a, b); break;
   }
   out[i] = r;
 }
@@ -695,7 +864,7 @@ __global__ void kat_kernel(int64_t ncol, const double* __restrict__ y0, int32_t 
   const P fun{};
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (i >= ncol) return;
-  Lane<P> L;
+  Lane<P, KRegs<P::NV>> L;
 #pragma unroll
   for (int v = 0; v < NV; ++v) L.y[v] = y0[v * ncol + i];
   L.t = teval[0];
@@ -706,7 +875,7 @@ __global__ void kat_kernel(int64_t ncol, const double* __restrict__ y0, int32_t 
   int64_t nacc = 0, nrej = 0;
   for (int v = 0; v < NV; ++v) out[(i * nt) * NV + v] = L.y[v];
   for (int it = 1; it < nt; ++it) {
-    while (!L.iterate(fun, teval[it], min_step, rtol, atol, nacc, nrej)) {
+    while (L.iterate(fun, teval[it], min_step, rtol, atol, nacc, nrej) == Lane<P, KRegs<P::NV>>::kStep) {
     }
     for (int v = 0; v < NV; ++v) out[(i * nt + it) * NV + v] = L.y[v];
   }
@@ -755,6 +924,17 @@ unsigned grid_for(int64_t n, int block) {
   if (b < 1) b = 1;
   if (b > 65535LL * 32) b = 65535LL * 32;
   return (unsigned)b;
+}
+
+int compute_units() {
+  static int cached = 0;
+  if (cached) return cached;
+  int dev = 0, ncu = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 1)
+    ncu = 256;
+  cached = ncu;
+  return cached;
 }
 
 int persistent_blocks() {
@@ -847,9 +1027,9 @@ rwrt_status rwrt_rk45_init(const rwrt_grid* g, const double* d_packed, int64_t n
 
 rwrt_status rwrt_rk45_run(const rwrt_grid* g, const double* d_packed, int64_t nray,
                           const rwrt_params* p, const double* d_tbound, int32_t it_begin,
-                          int32_t it_end, const int64_t* d_order, double* d_state,
-                          int64_t* d_count, int32_t* d_nanrow, double* d_out, int32_t* d_work,
-                          void* stream) {
+                          int32_t it_end, const int64_t* d_order, int64_t n_heavy,
+                          double* d_state, int64_t* d_count, int32_t* d_nanrow, double* d_out,
+                          int32_t* d_work, void* stream) {
   Field F;
   if (rwrt_status s = make_field(g, d_packed, F)) return s;
   if (!p) return fail(RWRT_ERR_ARG, "params is NULL%s");
@@ -861,13 +1041,18 @@ rwrt_status rwrt_rk45_run(const rwrt_grid* g, const double* d_packed, int64_t nr
   if (reinterpret_cast<uintptr_t>(d_out) % 16 != 0)
     return fail(RWRT_ERR_ARG, "output rows must be 16-byte aligned%s");
   if (nray == 0) return RWRT_OK;
-  if (hipMemsetAsync(d_work, 0, sizeof(int32_t), (hipStream_t)stream) != hipSuccess)
+  if (n_heavy < 0 || n_heavy > nray) return fail(RWRT_ERR_ARG, "n_heavy out of range%s");
+  if (hipMemsetAsync(d_work, 0, 2 * sizeof(int32_t), (hipStream_t)stream) != hipSuccess)
     return check_launch("hipMemsetAsync(queue)");
-  RunArgs a{F, nray, p->rtol, p->atol, p->min_step, p->cut_off, p->nt, it_begin, it_end,
-            d_tbound, d_order, d_state, d_count, d_nanrow, d_out, d_work};
   int64_t blocks = persistent_blocks();
   const int64_t need = (nray + 255) / 256;
   if (blocks > need) blocks = need;
+  // one high-priority block per CU when at least two blocks share each CU
+  const int ncu = compute_units();
+  const int heavy_blocks = (d_order && n_heavy > 0 && blocks >= 2 * (int64_t)ncu) ? ncu : 0;
+  RunArgs a{F, nray, p->rtol, p->atol, p->min_step, p->cut_off, p->nt, it_begin, it_end,
+            d_tbound, d_order, d_state, d_count, d_nanrow, d_out, d_work,
+            heavy_blocks ? n_heavy : 0, heavy_blocks};
   hipLaunchKernelGGL(rk45_run_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
   return check_launch("rk45_run_kernel");
 }
@@ -889,7 +1074,7 @@ rwrt_status rwrt_kat_rk45(int32_t kind, int64_t ncol, const double* d_y0, int32_
 
 rwrt_status rwrt_selftest_math(int32_t kind, int64_t n, const double* d_x, const double* d_y,
                                double* d_out, void* stream) {
-  if (n < 0 || kind < 0 || kind > 8 || (n > 0 && (!d_x || !d_out)))
+  if (n < 0 || kind < 0 || kind > 12 || (n > 0 && (!d_x || !d_out)))
     return fail(RWRT_ERR_ARG, "bad selftest arguments%s");
   if (n == 0) return RWRT_OK;
   hipLaunchKernelGGL(math_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, kind,

@@ -136,17 +136,35 @@ class RayEngine:
         dead = (st["live"] == 0).to(torch.int8)
         return torch.sort(dead, stable=True).indices.to(torch.int64).contiguous()
 
-    def run(self, st, p, tbound, it_begin, it_end, out, order=None):
+    @staticmethod
+    def cost_order(st, work):
+        """Longest-first queue order for the next chunk.
+
+        ``work`` = attempts each ray made in the previous chunk (a good predictor
+        of the next one: step sizes change slowly).  Frozen rays (NaN mean; one
+        row computation each) go last, where they fill the tail of the launch.
+        """
+        y = st["state"][:5]
+        frozen = torch.isnan(y.sum(0))
+        key = torch.where(frozen, torch.full_like(work, -1), work)
+        return torch.sort(key, descending=True, stable=True).indices.to(torch.int64).contiguous()
+
+    def heavy_lanes(self):
+        """Lanes of the high-priority waves (one 256-thread block per CU)."""
+        return torch.cuda.get_device_properties(self.device).multi_processor_count * 256
+
+    def run(self, st, p, tbound, it_begin, it_end, out, order=None, n_heavy=0):
         """Rows ``[it_begin, it_end)`` into ``out[nray, it_end-it_begin, 8]`` (async)."""
         H.check(H.load().rwrt_rk45_run(
             self.grid, H.dptr(self.packed), st["nray"], ctypes_ref(p), H.dptr(tbound, F64),
-            int(it_begin), int(it_end), H.dptr(order, torch.int64), H.dptr(st["state"]),
+            int(it_begin), int(it_end), H.dptr(order, torch.int64), int(n_heavy),
+            H.dptr(st["state"]),
             H.dptr(st["count"]), H.dptr(st["nanrow"]), H.dptr(out, F64), H.dptr(self.work),
             H.stream()))
 
     def integrate(self, y0, nt, tstep, rtol=1e-6, atol=1e-6, msf=1e-3, cut_off=0.1,
                   ttotal=None, chunk=None, sink=None, out=None, cut_rad=None, events=None,
-                  group=None):
+                  group=None, order_policy="priority", first_chunk=None):
         """The whole ray loop for ``y0[5, nray]``; rows 1..nt-1 go to ``sink``.
 
         ``sink(i0, i1, rows)`` receives each time chunk as a device tensor
@@ -175,21 +193,35 @@ class RayEngine:
             return RunResult(cnt[:, 0], cnt[:, 1], st["nanrow"], True, 1, n_live)
         order = self.live_first_order(st)
         chunk = chunk or (nt - 1)
-        if out is None or out.shape[0] != nray or out.shape[1] < min(chunk, nt - 1):
-            out = torch.empty((nray, min(chunk, nt - 1), H.NOUT), dtype=F64, device=self.device)
-        for i0 in range(1, nt, chunk):
-            i1 = min(i0 + chunk, nt)
-            view = out[:, : i1 - i0] if i1 - i0 < out.shape[1] else out
-            if not view.is_contiguous():
-                view = torch.empty((nray, i1 - i0, H.NOUT), dtype=F64, device=self.device)
+        bounds = []
+        i0 = 1
+        if first_chunk and order_policy in ("cost", "priority") and first_chunk < chunk:
+            bounds.append((1, min(1 + first_chunk, nt)))    # a short chunk to measure ray costs
+            i0 = bounds[-1][1]
+        while i0 < nt:
+            bounds.append((i0, min(i0 + chunk, nt)))
+            i0 = bounds[-1][1]
+        rows_max = max(b - a for a, b in bounds)
+        prev_work = None
+        if out is None or out.shape[0] != nray or out.shape[1] * out.shape[2] < rows_max * H.NOUT:
+            out = torch.empty((nray, rows_max, H.NOUT), dtype=F64, device=self.device)
+        flat = out.view(-1)
+        for i0, i1 in bounds:
+            view = flat[: nray * (i1 - i0) * H.NOUT].view(nray, i1 - i0, H.NOUT)
+            n_heavy = 0
+            if order_policy in ("cost", "priority") and prev_work is not None:
+                order = self.cost_order(st, cnt.sum(1) - prev_work)
+                if order_policy == "priority":
+                    n_heavy = min(self.heavy_lanes(), n_live)
+            prev_work = cnt.sum(1)
             if events is not None:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
-                self.run(st, p, tb, i0, i1, view, order)
+                self.run(st, p, tb, i0, i1, view, order, n_heavy)
                 e1.record()
                 events.append((e0, e1))
             else:
-                self.run(st, p, tb, i0, i1, view, order)
+                self.run(st, p, tb, i0, i1, view, order, n_heavy)
             if sink is not None:
                 sink(i0, i1, view)
         mx = int(st["nanrow"].max().item()) if nray else 0
@@ -219,7 +251,8 @@ def kat_rk45(kind, y0, t_eval, rtol, atol, min_step, device="cuda"):
 
 
 MATH_KINDS = {"sin": 0, "cos": 1, "tan": 2, "pow": 3, "atan2": 4, "mod": 5, "sqrt": 6,
-              "div": 7, "floor": 8}
+              "div": 7, "floor": 8, "sincos_sin": 9, "sincos_cos": 10, "div_rearth": 11,
+              "fmod": 12}
 
 
 def selftest_math(name, x, y=None, device="cuda"):

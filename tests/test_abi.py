@@ -38,6 +38,6 @@ def test_argument_errors_are_reported_without_a_gpu():
     assert b"grid" in lib.rwrt_last_error()
     g = H.Grid(145, 73, 0.0, 0.04363323, -1.5707964, 0.04363323)
     p = H.Params(1e-6, 1e-6, 7.2, 0.2, 1081, 0)
-    st = lib.rwrt_rk45_run(ctypes.byref(g), 16, 10, ctypes.byref(p), None, 0, 5, None, None,
-                           None, None, None, None, None)
+    st = lib.rwrt_rk45_run(ctypes.byref(g), 16, 10, ctypes.byref(p), None, 0, 5, None, 0,
+                           None, None, None, None, None, None)
     assert st == H.RWRT_ERR_ARG

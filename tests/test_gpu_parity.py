@@ -291,6 +291,24 @@ def test_device_math_exactness():
     assert np.array_equal(selftest_math("mod", lon, np.full(lon.shape, 2 * np.pi)),
                           lon % (2 * np.pi))
     lat = rng.uniform(-1.5707963, 1.5707963, n)
+    # the kernels' shortcuts are bit-identical to the operations they replace
+    assert np.array_equal(selftest_math("sincos_sin", lat), selftest_math("sin", lat))
+    assert np.array_equal(selftest_math("sincos_cos", lat), selftest_math("cos", lat))
+    wide = rng.standard_normal(4 * n) * 10.0 ** rng.uniform(-300, 300, 4 * n)
+    wide = np.concatenate([wide, [0.0, -0.0, np.inf, -np.inf, np.nan, 5e-324, -1e-310,
+                                  1.7e308, 6.3712e6, -6.3712e6 * 3]])
+    with np.errstate(all="ignore"):
+        assert np.array_equal(selftest_math("div_rearth", wide), wide / 6.3712e6, equal_nan=True)
+    phys = rng.standard_normal(4 * n) * 10.0 ** rng.uniform(-12, 4, 4 * n)
+    assert np.array_equal(selftest_math("div_rearth", phys), phys / 6.3712e6)
+    tp = 2 * np.pi
+    near = np.concatenate([np.arange(-200, 200) * tp, np.nextafter(np.arange(-200, 200) * tp, np.inf),
+                           np.nextafter(np.arange(-200, 200) * tp, -np.inf),
+                           rng.uniform(-1e4, 1e4, n), rng.uniform(-1e13, 1e13, 1000),
+                           [1e300, -1e300, np.inf, np.nan, 0.0, -0.0]])
+    with np.errstate(all="ignore"):
+        assert np.array_equal(selftest_math("fmod", near, np.full(near.shape, tp)),
+                              np.fmod(near, tp), equal_nan=True)
     rates = {}
     for name in ("sin", "cos", "tan"):
         rates[name] = float(np.mean(selftest_math(name, lat) != getattr(np, name)(lat)))
