@@ -78,6 +78,21 @@ def cpu_baseline(bg, y0, nrays, days, seed=0):
     return pick, hist, int(nacc.sum()), dt, nt
 
 
+def find_traffic(path, workload):
+    """Per-launch HBM bytes of the ray kernel from a PMC profile of this workload."""
+    import glob
+    cands = [path] if path else sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "traffic.json")),
+                                       key=os.path.getmtime, reverse=True)
+    for c in cands:
+        try:
+            t = json.load(open(c))
+        except (OSError, ValueError):
+            continue
+        if t.get("workload") == workload:
+            return t, os.path.relpath(c, ROOT)
+    return None, None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -95,6 +110,9 @@ def main():
     ap.add_argument("--first-chunk", type=int, default=6,
                     help="rows of the short first launch that measures per-ray cost")
     ap.add_argument("--lib", default=None, help="alternative librwrt build (A/B timing)")
+    ap.add_argument("--traffic", default=None,
+                    help="traffic.json from tools/pmc_traffic.py (default: newest profiles/*/traffic.json "
+                         "for this workload)")
     ap.add_argument("--replicate", type=int, default=1,
                     help="diagnostic: repeat the ray batch k times (more rays per lane)")
     args = ap.parse_args()
@@ -166,13 +184,15 @@ def main():
         per_launch_steps = steps_done / max(len(events), 1)
         avg_launch_s = kern_s / max(len(events), 1)
         achieved = per_launch_steps * BYTES_PER_STEP / avg_launch_s
+        workload = (f"C3: 2deg global seeds x k=1..10 x {args.periods} periods, "
+                    f"{args.days:g} d at 2 h, 2.5deg DJF jet background (BASELINE configs[2])")
+        traffic, tsrc = find_traffic(args.traffic, workload)
         result = {
             "metric": METRIC, "value": value, "unit": "ray-steps/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": 1e3 * max_el / args.steps, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-            "config": {"workload": f"C3: 2deg global seeds x k=1..10 x {args.periods} periods, "
-                                   f"{args.days:g} d at 2 h, 2.5deg DJF jet background (BASELINE configs[2])",
+            "config": {"workload": workload,
                        "ray_slots_per_gpu": nslot, "live_rays_per_gpu": n_live, "rows": nt,
                        "rows_per_launch": chunk, "parallelism": f"rays sharded, {world} rank(s), 1 GPU each"},
             "ray_steps_per_step": steps_done / args.steps,
@@ -181,7 +201,11 @@ def main():
             "queue_order": args.order,
             "library": os.path.basename(os.environ.get("RWRT_LIB", "librwrt.so")),
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK, "traffic": None,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK,
+                         "traffic": traffic["traffic_bytes_per_launch"] if traffic else None,
+                         "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
+                         "traffic_source": tsrc,
+                         "algorithmic_bytes_per_launch": per_launch_steps * BYTES_PER_STEP,
                          "kernel": "rk45_run_kernel", "avg_launch_ms": 1e3 * avg_launch_s,
                          "launches": len(events), "bytes_per_ray_step": BYTES_PER_STEP},
         }

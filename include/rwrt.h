@@ -59,6 +59,7 @@ typedef struct {
   double cut_off;   /* jump mask threshold, rad    wr.py:170       */
   int32_t nt;       /* rows of the history         wr.py:157       */
   int32_t reserved;
+  double tstep;     /* output interval = RK4 step  wr.py:147       */
 } rwrt_params;
 
 const char* rwrt_version(void);
@@ -126,6 +127,20 @@ rwrt_status rwrt_rk45_run(const rwrt_grid* g, const double* d_packed,
                           int64_t n_heavy, double* d_state, int64_t* d_count,
                           int32_t* d_nanrow, double* d_out, int32_t* d_work,
                           void* stream);
+
+/* Fixed-step RK4 ray loop, the reference's default integrator:
+ * WR.core_ray_run_numpy (wr.py:702-765) with rk4_step_numpy (wr.py:583-622)
+ * and core_rk4_step (wr.py:89-95), for rows it_begin <= i < it_end, dt =
+ * p->tstep.  A ray whose stage input is masked (|lat| >= pi/2 or |l| >= 100)
+ * keeps its state for that step.  d_state rows 0..4 hold y (set them to the
+ * initial rows before the first call); d_count[nray][2] = {steps taken, steps
+ * held}; d_nanrow / d_out / d_work as for rwrt_rk45_run (nacc column = steps
+ * taken). */
+rwrt_status rwrt_rk4_run(const rwrt_grid* g, const double* d_packed,
+                         int64_t nray, const rwrt_params* p, int32_t it_begin,
+                         int32_t it_end, const int64_t* d_order,
+                         double* d_state, int64_t* d_count, int32_t* d_nanrow,
+                         double* d_out, int32_t* d_work, void* stream);
 
 /* Stepper known-answer tests: the same device stepper on the analytic ODEs of
  * the rkf45.py demos (rkf45.py:839-882), driven like rk45_simple_current

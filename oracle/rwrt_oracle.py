@@ -536,3 +536,76 @@ def run_config(bg, cfg, nt=None):
     row0 = np.array(rows).reshape(7, -1)
     return ray_run(bg, y0, nt, tstep, cfg.rtol, cfg.atol, cfg.MinStepFactor,
                    ttotal=cfg.ttotal * DAY, row0=row0)
+
+
+# ----------------------------------------------------------------------------
+# fixed-step RK4 (the reference's default integrator, inte_method='')
+# ----------------------------------------------------------------------------
+def rhs7(bg, y):
+    """``diffun_numpy`` with all 7 outputs: (dlon, dlat, dk, dl, damp, ug/R, vg).
+
+    ``core_diffun`` (wr.py:68-81) aliases ``dlon = ug`` and divides it in place,
+    so the returned ``dug`` is ``ug / R`` while ``dvg`` is ``vg`` itself.
+    Returns ``(d[7, N], bad[N])``.
+    """
+    d5, bad = rhs(bg, y[:5])
+    lat, ky, kx = y[1], y[3].copy(), y[2]
+    ky[bad] = np.nan
+    M = mercator_point(bg, y[0].reshape(-1), lat.reshape(-1))
+    ug, vg = ugvg_extent(M[0], M[1], M[6], M[7], kx, ky)
+    d = np.concatenate([d5, (ug / R_EARTH)[None], vg[None]], axis=0)
+    d[5:, bad] = np.nan
+    return d, bad
+
+
+def ray_run_rk4(bg, y0, nt, tstep, cut_off=0.1, row0=None):
+    """``core_ray_run_numpy`` (wr.py:702-765) with ``rk4_step_numpy`` (wr.py:583-622).
+
+    Rays where any of the four stage inputs is masked (|lat| >= pi/2 or
+    |l| >= 100) keep their state for that step (wr.py:609-618); NaN states
+    are not masked and propagate.  Returns ``(hist[7, nt, nray], status)``.
+    """
+    nray = y0.shape[1]
+    hist = np.full((7, nt, nray), np.nan)
+    if row0 is not None:
+        hist[:, 0] = row0
+    else:
+        hist[:5, 0] = y0
+    dt = np.array([tstep], dtype=np.float64)
+    cut = cut_off * dt / 3600.0
+    y = np.array(hist[:, 0])
+    for it in range(nt - 1):
+        k1, m1 = rhs7(bg, y)
+        y_next = y.copy()
+        valid1 = ~m1
+        if np.any(valid1):
+            k2, m2 = rhs7(bg, y + 0.5 * dt * k1)
+            k3, m3 = rhs7(bg, y + 0.5 * dt * k2)
+            k4, m4 = rhs7(bg, y + dt * k3)
+            ok = valid1 & ~m2 & ~m3 & ~m4
+            ks = (dt / 6.0) * (k1 + 2 * k2 + 2 * k3 + k4)          # core_rk4_step wr.py:89-95
+            prop = y.copy()
+            prop[0:5] = y[0:5] + ks[0:5]
+            prop[5:] = ks[5:] / dt
+            y_next[:, ok] = prop[:, ok]
+        yn = y_next
+        yn[:5, np.abs(yn[1]) >= 0.5 * PI] = np.nan                     # wr.py:721-726
+        yn[:5, np.abs(cal_dis(yn[0], yn[1], hist[0, it], hist[1, it])) >= cut] = np.nan
+        if np.isnan(yn[0]).all() or (np.abs(yn[1]) > 0.5 * PI).all():  # wr.py:735-736
+            break
+        M = mercator_point(bg, yn[0], yn[1])
+        ug, vg = ugvg_extent(M[0], M[1], M[6], M[7], yn[2], yn[3])
+        hist[:5, it + 1] = yn[:5]
+        hist[5, it + 1], hist[6, it + 1] = ug, vg
+        y = np.array(hist[:, it + 1])
+    return hist, 0
+
+
+def run_config_rk4(bg, cfg, nt=None):
+    slon, slat = source_matrix(cfg.SW_lon, cfg.SW_lat, cfg.dlon, cfg.dlat, cfg.nnx, cfg.nny)
+    rows = ray_initial(bg, slon, slat, cfg.zwn, cfg.freq)
+    tstep = cfg.tstep * HOUR
+    if nt is None:
+        nt = int(cfg.ttotal * DAY / tstep) + 1
+    row0 = np.array(rows).reshape(7, -1)
+    return ray_run_rk4(bg, row0[:5].copy(), nt, tstep, row0=row0)

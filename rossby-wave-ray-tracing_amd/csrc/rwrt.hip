@@ -855,6 +855,104 @@ __global__ void math_kernel(int kind, int64_t n, const double* __restrict__ x,
   out[i] = r;
 }
 
+// ---------------------------------------------------------------------------
+// Fixed-step RK4: WR.core_ray_run_numpy (wr.py:702-765) + rk4_step_numpy
+// (wr.py:583-622) + core_rk4_step (wr.py:89-95), the reference's default
+// integrator (inte_method='').  Same RHS, same post-processing.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool rhs_bad(const double* y) {
+  return fabs(y[1]) >= kHalfPi || fabs(y[3]) >= 100.0;   // diffun_numpy err_mask (wr.py:508-510)
+}
+
+struct Rk4Args {
+  Field F;
+  int64_t nray;
+  double dt, cut_off;
+  int32_t nt, it_begin, it_end;
+  const int64_t* order;
+  double* state;      // rows 0..4 of the [12][nray] state: y
+  int64_t* count;     // [nray][2]: steps taken, steps held (a masked stage)
+  int32_t* nanrow;
+  double* out;
+  int32_t* queue;
+};
+
+__global__ void __launch_bounds__(256, RWRT_WAVES_PER_SIMD) rk4_run_kernel(Rk4Args a) {
+  const int64_t nrows = a.it_end - a.it_begin;
+  const double half = 0.5 * a.dt;        // 0.5 * dt      (wr.py:602-604)
+  const double sixth = a.dt / 6.0;       // dt / 6.0      (wr.py:92)
+  for (;;) {
+    const int32_t w = atomicAdd(a.queue, 1);
+    if (w >= a.nray) break;
+    const int64_t ray = a.order ? a.order[w] : (int64_t)w;
+    double y[5];
+#pragma unroll
+    for (int v = 0; v < 5; ++v) y[v] = a.state[v * a.nray + ray];
+    int64_t nstep = a.count[2 * ray], nhold = a.count[2 * ray + 1];
+    int32_t nanrow = a.nanrow[ray];
+    double prev_lon = y[0], prev_lat = y[1];
+    int it = a.it_begin;
+    while (it < a.it_end) {
+      // one RK4 step: k1 at y; k2, k3 at y + dt/2 k; k4 at y + dt k3 (one RHS copy)
+      const bool bad1 = rhs_bad(y);
+      bool held = bad1;
+      double acc[5], k[5], ys[5];
+#pragma nounroll
+      for (int s = 0; s < 4; ++s) {
+        const double c = (s == 3) ? a.dt : half;
+#pragma unroll
+        for (int v = 0; v < 5; ++v) ys[v] = (s == 0) ? y[v] : y[v] + c * k[v];
+        if (s > 0 && rhs_bad(ys)) held = true;
+        ray_rhs(a.F, ys, k);
+        const double wgt = (s == 1 || s == 2) ? 2.0 : 1.0;
+#pragma unroll
+        for (int v = 0; v < 5; ++v) acc[v] = (s == 0) ? k[v] : acc[v] + wgt * k[v];
+        if (bad1) break;   // wr.py:600: no later stage matters for this ray
+      }
+      if (!held) {
+#pragma unroll
+        for (int v = 0; v < 5; ++v) y[v] = y[v] + sixth * acc[v];
+        ++nstep;
+      } else if (!bad1) {
+        ++nhold;
+      }
+      // post-processing (wr.py:718-756)
+      if (fabs(y[1]) >= kHalfPi) {
+#pragma unroll
+        for (int v = 0; v < 5; ++v) y[v] = kNaN;
+      }
+      if (cal_dis(y[0], y[1], prev_lon, prev_lat) >= a.cut_off) {
+#pragma unroll
+        for (int v = 0; v < 5; ++v) y[v] = kNaN;
+      }
+      double ug, vg;
+      ugvg_at(a.F, y[0], y[1], y[2], y[3], ug, vg);
+      const double2 r0 = make_double2(y[0], y[1]), r1 = make_double2(y[2], y[3]);
+      const double2 r2 = make_double2(y[4], ug), r3 = make_double2(vg, (double)nstep);
+      // A held ray (masked first stage) or an all-NaN state repeats this row
+      // forever: write every remaining row of the chunk at once.
+      const bool allnan = isnan(y[0]) && isnan(y[1]) && isnan(y[2]) && isnan(y[3]) && isnan(y[4]);
+      const int last = (bad1 || allnan) ? a.it_end : it + 1;
+      for (int q = it; q < last; ++q) {
+        double2* o = reinterpret_cast<double2*>(a.out + ((size_t)ray * nrows + (q - a.it_begin)) * RWRT_NOUT);
+        o[0] = r0;
+        o[1] = r1;
+        o[2] = r2;
+        o[3] = r3;
+      }
+      if (nanrow == a.nt && isnan(y[0])) nanrow = it;
+      prev_lon = y[0];
+      prev_lat = y[1];
+      it = last;
+    }
+#pragma unroll
+    for (int v = 0; v < 5; ++v) a.state[v * a.nray + ray] = y[v];
+    a.count[2 * ray] = nstep;
+    a.count[2 * ray + 1] = nhold;
+    a.nanrow[ray] = nanrow;
+  }
+}
+
 // rk45_simple_current (rkf45.py:672-724) over ncol columns, one lane each.
 template <class P>
 __global__ void kat_kernel(int64_t ncol, const double* __restrict__ y0, int32_t nt,
@@ -1055,6 +1153,33 @@ rwrt_status rwrt_rk45_run(const rwrt_grid* g, const double* d_packed, int64_t nr
             heavy_blocks ? n_heavy : 0, heavy_blocks};
   hipLaunchKernelGGL(rk45_run_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
   return check_launch("rk45_run_kernel");
+}
+
+rwrt_status rwrt_rk4_run(const rwrt_grid* g, const double* d_packed, int64_t nray,
+                         const rwrt_params* p, int32_t it_begin, int32_t it_end,
+                         const int64_t* d_order, double* d_state, int64_t* d_count,
+                         int32_t* d_nanrow, double* d_out, int32_t* d_work, void* stream) {
+  Field F;
+  if (rwrt_status s = make_field(g, d_packed, F)) return s;
+  if (!p) return fail(RWRT_ERR_ARG, "params is NULL%s");
+  if (nray < 0 || nray > 0x7fffffffLL) return fail(RWRT_ERR_ARG, "nray out of range%s");
+  if (it_begin < 1 || it_end > p->nt || it_begin >= it_end)
+    return fail(RWRT_ERR_ARG, "need 1 <= it_begin < it_end <= nt%s");
+  if (!(p->tstep > 0.0)) return fail(RWRT_ERR_ARG, "tstep must be positive%s");
+  if (!d_state || !d_count || !d_nanrow || !d_out || !d_work)
+    return fail(RWRT_ERR_ARG, "NULL buffer to rwrt_rk4_run%s");
+  if (reinterpret_cast<uintptr_t>(d_out) % 16 != 0)
+    return fail(RWRT_ERR_ARG, "output rows must be 16-byte aligned%s");
+  if (nray == 0) return RWRT_OK;
+  if (hipMemsetAsync(d_work, 0, sizeof(int32_t), (hipStream_t)stream) != hipSuccess)
+    return check_launch("hipMemsetAsync(queue)");
+  Rk4Args a{F, nray, p->tstep, p->cut_off, p->nt, it_begin, it_end, d_order, d_state, d_count,
+            d_nanrow, d_out, d_work};
+  int64_t blocks = persistent_blocks();
+  const int64_t need = (nray + 255) / 256;
+  if (blocks > need) blocks = need;
+  hipLaunchKernelGGL(rk4_run_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
+  return check_launch("rk4_run_kernel");
 }
 
 rwrt_status rwrt_kat_rk45(int32_t kind, int64_t ncol, const double* d_y0, int32_t nt,

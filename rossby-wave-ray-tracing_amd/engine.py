@@ -111,7 +111,7 @@ class RayEngine:
         tstep = float(tstep)
         min_step = min(msf * tstep, (tstep - 0) * 0.001)          # rkf45.py:362, wr.py:792-794
         cut = cut_off * tstep / 3600.0 if cut_rad is None else float(cut_rad)   # wr.py:170
-        return H.Params(rtol, atol, min_step, cut, int(nt), 0)
+        return H.Params(rtol, atol, min_step, cut, int(nt), 0, tstep)
 
     def init(self, y0, p):
         """Solver construction on the GPU; returns the per-ray state tensors."""
@@ -161,6 +161,52 @@ class RayEngine:
             H.dptr(st["state"]),
             H.dptr(st["count"]), H.dptr(st["nanrow"]), H.dptr(out, F64), H.dptr(self.work),
             H.stream()))
+
+    def integrate_rk4(self, y0, nt, tstep, cut_off=0.1, chunk=None, sink=None, out=None,
+                      cut_rad=None, events=None, group=None):
+        """The fixed-step RK4 ray loop (wr.py:702-765) for ``y0[5, nray]``.
+
+        Same chunked ``sink`` protocol as ``integrate``; the nacc column and
+        ``RunResult.nacc`` count RK4 steps taken, ``nrej`` steps held because a
+        stage input was masked (the ray keeps its state, wr.py:609-618).
+        """
+        p = self.params(nt, tstep, cut_off=cut_off, cut_rad=cut_rad)
+        y0 = torch.as_tensor(y0, dtype=F64, device=self.device).contiguous()
+        nray = y0.shape[1]
+        st = dict(state=torch.empty((H.NSTATE, nray), dtype=F64, device=self.device),
+                  count=torch.zeros((nray, 2), dtype=torch.int64, device=self.device),
+                  nanrow=torch.full((nray,), int(nt), dtype=torch.int32, device=self.device),
+                  nray=nray)
+        st["state"][:5] = y0
+        live = ~torch.isnan(y0.sum(0))
+        order = torch.sort((~live).to(torch.int8), stable=True).indices.to(torch.int64).contiguous()
+        chunk = chunk or (nt - 1)
+        rows_max = min(chunk, nt - 1)
+        if out is None or out.numel() < nray * rows_max * H.NOUT:
+            out = torch.empty((nray, rows_max, H.NOUT), dtype=F64, device=self.device)
+        flat = out.reshape(-1)
+        for i0 in range(1, nt, chunk):
+            i1 = min(i0 + chunk, nt)
+            view = flat[: nray * (i1 - i0) * H.NOUT].view(nray, i1 - i0, H.NOUT)
+            if events is not None:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+            H.check(H.load().rwrt_rk4_run(
+                self.grid, H.dptr(self.packed), nray, ctypes_ref(p), int(i0), int(i1),
+                H.dptr(order, torch.int64), H.dptr(st["state"]), H.dptr(st["count"]),
+                H.dptr(st["nanrow"]), H.dptr(view, F64), H.dptr(self.work), H.stream()))
+            if events is not None:
+                e1.record()
+                events.append((e0, e1))
+            if sink is not None:
+                sink(i0, i1, view)
+        mx = int(st["nanrow"].max().item()) if nray else 0
+        if group is not None:
+            from shard import reduce_max
+            mx = reduce_max(mx, group)
+        cnt = st["count"]
+        return RunResult(cnt[:, 0], cnt[:, 1], st["nanrow"], False, mx if mx < nt else None,
+                         int(live.sum().item()))
 
     def integrate(self, y0, nt, tstep, rtol=1e-6, atol=1e-6, msf=1e-3, cut_off=0.1,
                   ttotal=None, chunk=None, sink=None, out=None, cut_rad=None, events=None,

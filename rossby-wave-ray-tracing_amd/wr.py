@@ -19,7 +19,7 @@ from constants import day, hour, rad2deg, undef, deg2rad
 import ncio
 from wn import cal_ugvg
 
-SUPPORTED = ("hip_rk45",)
+SUPPORTED = ("hip_rk45", "hip")      # GPU RK45 (wr.py:767-887) and GPU RK4 (wr.py:702-765)
 
 
 def progress_bar(current, total, bar_length=50):
@@ -131,7 +131,15 @@ class WR:
 
     # ---------------------------------------------------------- ray loop
     def core_ray_run_hip_rk45(self, group=None):
-        """The RK45 ray loop on the GPU (replaces wr.py:767-887).
+        """The RK45 ray loop on the GPU (replaces wr.py:767-887)."""
+        return self._core_ray_run_hip("rk45", group)
+
+    def core_ray_run_hip(self, group=None):
+        """The fixed-step RK4 ray loop on the GPU (replaces wr.py:702-765)."""
+        return self._core_ray_run_hip("rk4", group)
+
+    def _core_ray_run_hip(self, method, group=None):
+        """Shared driver of the two GPU ray loops.
 
         With a torch.distributed ``group`` of one process per GPU, the rays are
         sharded over the ranks (shard.py): rank 0's basic state is broadcast,
@@ -166,10 +174,15 @@ class WR:
                 progress_bar(i1 - 1, self.nt)
 
         chunk = self.chunk_rows or _default_chunk(nray, self.nt)
-        res = eng.integrate(torch.as_tensor(y0[:, idx]), self.nt, float(self.tstep[0]),
-                            self.rtol, self.atol, self.MinStepFactor, ttotal=self.ttotal,
-                            chunk=chunk, sink=sink, cut_rad=float(self.cut_off[0]),
-                            group=group if world > 1 else None)
+        grp = group if world > 1 else None
+        if method == "rk4":
+            res = eng.integrate_rk4(torch.as_tensor(y0[:, idx]), self.nt, float(self.tstep[0]),
+                                    chunk=chunk, sink=sink, cut_rad=float(self.cut_off[0]),
+                                    group=grp)
+        else:
+            res = eng.integrate(torch.as_tensor(y0[:, idx]), self.nt, float(self.tstep[0]),
+                                self.rtol, self.atol, self.MinStepFactor, ttotal=self.ttotal,
+                                chunk=chunk, sink=sink, cut_rad=float(self.cut_off[0]), group=grp)
         if res.break_row is not None:
             for h in hist:
                 h[res.break_row:] = np.nan     # rows never stored (wr.py:853-855, 886-887)
@@ -180,7 +193,10 @@ class WR:
         if mode not in SUPPORTED:
             raise NotImplementedError(
                 f"ray loop {mode!r} is not provided by this framework; use "
-                f"ray_run(mode='hip', inte_method='rk45') (the MI355X RK45 ray loop)")
+                f"ray_run(mode='hip', inte_method='rk45') (adaptive RK45) or "
+                f"ray_run(mode='hip', inte_method='') (fixed-step RK4) on the MI355X")
+        if mode == "hip":
+            return self.core_ray_run_hip(group=group)
         return self.core_ray_run_hip_rk45(group=group)
 
     def ray_run(self, mode="hip", inte_method="rk45", root_method="numpy", debug=False,

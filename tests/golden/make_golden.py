@@ -17,6 +17,9 @@ its own functions produce every expected value below:
 * ``traj_C2_<kind>.npz``  C2 history rows 1, 12, 120 (+ per-ray accepted steps)
 * ``roots_C3.npz``      initial rows on a C3 subsample (stationary, 10-day period)
 * ``kat_stepper.npz``   ``rk45_simple_current`` on the rkf45.py demo ODEs      (rkf45.py:672-724,825-882)
+* ``rk4_C1.npz``, ``rk4_C2_<kind>.npz``  the default fixed-step RK4 path,
+  ``ray_run(mode='numpy', inte_method='')`` (wr.py:583-622,702-765)
+  (``python tests/golden/make_golden.py --rk4-only`` regenerates just these)
 """
 import contextlib
 import hashlib
@@ -211,6 +214,20 @@ def run_traj(kind, name, nt, rows_keep=None):
                 attempts=np.array(sc.attempts), nt=np.array(nt), wall=np.array(dt))
 
 
+def run_traj_rk4(kind, name, nt, rows_keep=None):
+    bg = S.background(kind)
+    cfg = S.config(name, bg=kind)
+    cfg.ttotal = (nt - 1) * cfg.tstep / 24.0
+    wr = make_wr(bg, cfg, f"rk4_{name}_{kind}.nc")
+    t0 = time.time()
+    quiet(wr.ray_run, mode="numpy", inte_method="", root_method="numpy")
+    dt = time.time() - t0
+    hist = np.array([wr.rlon, wr.rlat, wr.rzwn, wr.rmwn, wr.ramp, wr.rug, wr.rvg]).reshape(7, nt, -1)
+    keep = np.arange(nt) if rows_keep is None else np.asarray(rows_keep)
+    print(f"rk4 {name} {kind}: nt={nt} {dt:.1f}s")
+    return dict(rows=keep, hist=hist[:, keep], nt=np.array(nt), wall=np.array(dt))
+
+
 def gen_roots():
     """Initial rows on a C3 subsample: every 17th source, stationary and 10-day period."""
     out = {}
@@ -269,6 +286,13 @@ def gen_kat():
     np.savez_compressed(os.path.join(HERE, "kat_stepper.npz"), **out)
 
 
+def main_rk4_only():
+    np.savez_compressed(os.path.join(HERE, "rk4_C1.npz"), **run_traj_rk4("zonal", "C1", 1081))
+    for kind in ["zonal", "nonzonal"]:
+        np.savez_compressed(os.path.join(HERE, f"rk4_C2_{kind}.npz"),
+                            **run_traj_rk4(kind, "C2", 121, rows_keep=[1, 12, 60, 120]))
+
+
 def main():
     rng = np.random.default_rng(20251015)
     for kind in ["zonal", "nonzonal"]:
@@ -281,8 +305,15 @@ def main():
         np.savez_compressed(os.path.join(HERE, f"traj_C2_{kind}.npz"), **c2)
     gen_roots()
     gen_kat()
+    np.savez_compressed(os.path.join(HERE, "rk4_C1.npz"), **run_traj_rk4("zonal", "C1", 1081))
+    for kind in ["zonal", "nonzonal"]:
+        np.savez_compressed(os.path.join(HERE, f"rk4_C2_{kind}.npz"),
+                            **run_traj_rk4(kind, "C2", 121, rows_keep=[1, 12, 60, 120]))
     print("done")
 
 
 if __name__ == "__main__":
-    main()
+    if "--rk4-only" in sys.argv:
+        main_rk4_only()
+    else:
+        main()

@@ -25,9 +25,9 @@ def test_library_exports_every_symbol():
 
 
 def test_struct_layouts():
-    # rwrt_grid: 2 x int32 + 4 x double; rwrt_params: 4 x double + 2 x int32
+    # rwrt_grid: 2 x int32 + 4 x double; rwrt_params: 4 x double + 2 x int32 + double
     assert ctypes.sizeof(H.Grid) == 40
-    assert ctypes.sizeof(H.Params) == 40
+    assert ctypes.sizeof(H.Params) == 48
 
 
 def test_argument_errors_are_reported_without_a_gpu():
@@ -37,7 +37,7 @@ def test_argument_errors_are_reported_without_a_gpu():
     assert st == H.RWRT_ERR_ARG
     assert b"grid" in lib.rwrt_last_error()
     g = H.Grid(145, 73, 0.0, 0.04363323, -1.5707964, 0.04363323)
-    p = H.Params(1e-6, 1e-6, 7.2, 0.2, 1081, 0)
+    p = H.Params(1e-6, 1e-6, 7.2, 0.2, 1081, 0, 7200.0)
     st = lib.rwrt_rk45_run(ctypes.byref(g), 16, 10, ctypes.byref(p), None, 0, 5, None, 0,
                            None, None, None, None, None, None)
     assert st == H.RWRT_ERR_ARG

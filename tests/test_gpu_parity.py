@@ -317,3 +317,47 @@ def test_device_math_exactness():
     print("device/NumPy last-bit mismatch rates:", rates)
     assert rates["sin"] < 0.05 and rates["cos"] < 0.05 and rates["tan"] < 0.1
     assert rates["pow"] < 0.2
+
+
+# ------------------------------------------------------------------- RK4 mode
+def run_wr(kind, cfg_name, nt, inte_method):
+    from wr import WR
+    cfg = S.config(cfg_name)
+    bs = bs_of(kind)
+    w = WR(cfg.nzwn, cfg.nsource, 7200.0, (nt - 1) * 7200.0, cfg.freq, nx=bs.nlon, ny=bs.nlat)
+    w.bs = bs
+    w.set_zwn(cfg.zwn)
+    w.set_source_matrix(cfg.SW_lon, cfg.SW_lat, cfg.dlon, cfg.dlat, cfg.nnx, cfg.nny)
+    with np.errstate(all="ignore"):
+        w.ray_run(mode="hip", inte_method=inte_method)
+    return np.array([w.rlon, w.rlat, w.rzwn, w.rmwn, w.ramp, w.rug, w.rvg]).reshape(7, nt, -1)
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_rk4_c2_tight(kind):
+    """Fixed-step RK4 has no step control to amplify last-bit differences:
+    the GPU stays within 1e-9 rad of the reference for 10 days (the
+    reference's own 1-ulp spread is ~1e-11)."""
+    g = golden(f"rk4_C2_{kind}.npz")
+    nt = int(g["nt"])
+    hist = run_wr(kind, "C2", nt, "")
+    ref = g["hist"]
+    for j, row in enumerate(g["rows"]):
+        a, b = hist[:, row], ref[:, j]
+        assert np.array_equal(np.isnan(a[0]), np.isnan(b[0])), row
+        ok = ~np.isnan(a[0]) & ~np.isnan(b[0])
+        d = np.max(np.abs(a[:2, ok] - b[:2, ok])) if ok.any() else 0.0
+        assert d <= 1e-9, (row, d)
+        for v in (2, 3, 4):
+            m = ~np.isnan(b[v]) & ~np.isnan(a[v])
+            assert np.allclose(a[v, m], b[v, m], rtol=1e-8, atol=1e-12), (row, v)
+
+
+def test_rk4_c1_90d():
+    g = golden("rk4_C1.npz")
+    nt = int(g["nt"])
+    hist = run_wr("zonal", "C1", nt, "")
+    ref = g["hist"]
+    assert np.array_equal(np.isnan(hist[0]), np.isnan(ref[0]))
+    ok = ~np.isnan(ref[0])
+    assert np.max(np.abs(hist[:2][:, ok] - ref[:2][:, ok])) <= 1e-6

@@ -145,3 +145,18 @@ def test_kat_lorenz():
         x, y, z = u
         return np.array([-p * x + p * y, -x * z + r * x - y, x * y - b * z])
     _kat("lorenz", lorenz)
+
+
+def test_rk4_c1_bitwise():
+    g = golden("rk4_C1.npz")
+    with np.errstate(all="ignore"):
+        hist, st = O.run_config_rk4(bg("zonal"), S.config("C1"), nt=int(g["nt"]))
+    assert same(hist, g["hist"])
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_rk4_c2_bitwise(kind):
+    g = golden(f"rk4_C2_{kind}.npz")
+    with np.errstate(all="ignore"):
+        hist, st = O.run_config_rk4(bg(kind), S.config("C2"), nt=int(g["nt"]))
+    assert same(hist[:, g["rows"]], g["hist"])
