@@ -10,11 +10,14 @@ The only expected differences are last-bit ones from the device's sin/cos/tan/
 pow/atan2 (the reference's NumPy uses glibc/SVML); every other operation is
 evaluated in the reference's order with IEEE division/sqrt and no FMA.
 """
+import json
+import os
+
 import numpy as np
 import pytest
 import torch
 
-from conftest import golden
+from conftest import GOLDEN, golden
 import synthetic as S
 
 pytestmark = pytest.mark.gpu
@@ -354,10 +357,19 @@ def test_rk4_c2_tight(kind):
 
 
 def test_rk4_c1_90d():
+    """90-day RK4 run of C1.  Last-bit differences stay below 1e-8 rad for 30
+    days; after that the zonal waveguide amplifies them, so the bound for the
+    remaining rows is twice the reference's own 1-ulp spread at 90 days
+    (tests/golden/noise_floor_C1_rk4_zonal.json, tools/noise_floor.py --rk4)."""
     g = golden("rk4_C1.npz")
     nt = int(g["nt"])
     hist = run_wr("zonal", "C1", nt, "")
     ref = g["hist"]
+    with open(os.path.join(GOLDEN, "noise_floor_C1_rk4_zonal.json")) as f:
+        floor90 = json.load(f)["90d"]["max"]
     assert np.array_equal(np.isnan(hist[0]), np.isnan(ref[0]))
     ok = ~np.isnan(ref[0])
-    assert np.max(np.abs(hist[:2][:, ok] - ref[:2][:, ok])) <= 1e-6
+    d = np.max(np.abs(hist[:2] - ref[:2]), axis=0, where=ok[None], initial=0.0)
+    d = d.max(axis=1)
+    assert d[:361].max() <= 1e-8, d[:361].max()
+    assert d.max() <= 2 * floor90, (d.max(), floor90)

@@ -6,7 +6,7 @@ of a last-bit difference in one transcendental.  The spread between the
 perturbed and the clean run is the floor below which no implementation that is
 not bit-identical to NumPy's libm/SVML can agree with the reference.
 
-    python tools/noise_floor.py [--kind zonal|nonzonal] [--days 10]
+    python tools/noise_floor.py [--kind zonal|nonzonal] [--days 10] [--config C2] [--rk4]
 """
 import argparse
 import json
@@ -21,9 +21,9 @@ import rwrt_oracle as O  # noqa: E402
 import synthetic as S    # noqa: E402
 
 
-def run(kind, nt, perturb_seed=None):
+def run(kind, nt, perturb_seed=None, config="C2", rk4=False):
     bg = O.Background(**S.background(kind))
-    cfg = S.config("C2")
+    cfg = S.config(config)
     slon, slat = O.source_matrix(cfg.SW_lon, cfg.SW_lat, cfg.dlon, cfg.dlat, cfg.nnx, cfg.nny)
     rows = np.array(O.ray_initial(bg, slon, slat, cfg.zwn, cfg.freq)).reshape(7, -1)
     orig = O.rhs
@@ -35,7 +35,10 @@ def run(kind, nt, perturb_seed=None):
             return d * (1 + rng.choice([-1.0, 1.0], d.shape) * 2.0 ** -52), bad
         O.rhs = rhs
     try:
-        hist, nacc, nrej, st = O.ray_run(bg, rows[:5].copy(), nt, 7200.0, row0=rows)
+        if rk4:
+            hist, st = O.ray_run_rk4(bg, rows[:5].copy(), nt, 7200.0, row0=rows)
+        else:
+            hist, nacc, nrej, st = O.ray_run(bg, rows[:5].copy(), nt, 7200.0, row0=rows)
     finally:
         O.rhs = orig
     return hist
@@ -45,13 +48,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--kind", default="nonzonal")
     ap.add_argument("--days", type=float, default=10.0)
+    ap.add_argument("--config", default="C2")
+    ap.add_argument("--rk4", action="store_true")
     a = ap.parse_args()
     nt = int(a.days * 12) + 1
     with np.errstate(all="ignore"):
-        h0 = run(a.kind, nt)
-        h1 = run(a.kind, nt, perturb_seed=1)
+        h0 = run(a.kind, nt, config=a.config, rk4=a.rk4)
+        h1 = run(a.kind, nt, perturb_seed=1, config=a.config, rk4=a.rk4)
     live = ~np.isnan(h0[3, 0])
-    out = {"kind": a.kind, "live_rays": int(live.sum())}
+    out = {"kind": a.kind, "config": a.config, "integrator": "rk4" if a.rk4 else "rk45",
+           "live_rays": int(live.sum())}
     for row in [1, 12, 24, 60, 120, 360, 1080]:
         if row >= nt:
             continue

@@ -1,17 +1,18 @@
 #!/bin/bash
 # Round profile on the GPU box: kernel-trace stats + FETCH/WRITE/SQ PMC passes
-# of the default bench command, summaries into profiles/<round>/.
+# of the bench command.  Raw output and summaries go to gpurun_out/prof_<round>/
+# (merged back by gpurun); copy the summary/ directory into profiles/<round>/.
 #   tools/profile_round.sh r1 [bench args]
 set -e
 r=$1; shift
 export TMPDIR=/tmp
-out=gpurun_out/prof_$r; mkdir -p $out profiles/$r
-B="python3 bench.py --steps 1 --warmup 0 --no-cpu $*"
+out=gpurun_out/prof_$r; sum=$out/summary; mkdir -p $out $sum
+B="python3 bench.py --steps 2 --warmup 1 --no-cpu $*"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/trace -o run --output-format csv -- $B > $out/trace.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $out/fetch -o run --output-format csv -- $B > $out/fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $out/write -o run --output-format csv -- $B > $out/write.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU --kernel-trace -d $out/sq -o run --output-format csv -- $B > $out/sq.log 2>&1
-cp $out/trace/run_kernel_stats.csv profiles/$r/kernel_stats.csv
-python3 tools/pmc_traffic.py $out/fetch $out/write $out/trace.log profiles/$r/traffic.json
-cp $out/sq/run_counter_collection.csv profiles/$r/sq_counters.csv
-grep -h '^{' $out/trace.log > profiles/$r/bench_under_rocprof.json || true
+cp $out/trace/run_kernel_stats.csv $sum/kernel_stats.csv
+python3 tools/pmc_traffic.py $out/fetch $out/write $out/trace.log $sum/traffic.json
+cp $out/sq/run_counter_collection.csv $sum/sq_counters.csv
+grep -h '^{' $out/trace.log > $sum/bench_under_rocprof.json || true
