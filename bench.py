@@ -78,8 +78,9 @@ def cpu_baseline(bg, y0, nrays, days, seed=0):
     return pick, hist, int(nacc.sum()), dt, nt
 
 
-def find_traffic(path, workload):
-    """Per-launch HBM bytes of the ray kernel from a PMC profile of this workload."""
+def find_traffic(path, workload, schedule):
+    """Per-launch HBM bytes of the ray kernel from a PMC profile of this workload
+    run with the same launch schedule (rows per launch)."""
     import glob
     cands = [path] if path else sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "traffic.json")),
                                        key=os.path.getmtime, reverse=True)
@@ -88,7 +89,7 @@ def find_traffic(path, workload):
             t = json.load(open(c))
         except (OSError, ValueError):
             continue
-        if t.get("workload") == workload:
+        if t.get("workload") == workload and t.get("launch_rows") == schedule:
             return t, os.path.relpath(c, ROOT)
     return None, None
 
@@ -107,8 +108,8 @@ def main():
     ap.add_argument("--order", default="priority", choices=["priority", "cost", "live"],
                     help="work-queue order: heaviest rays to high-priority waves (priority), "
                          "longest-first (cost), or live-first")
-    ap.add_argument("--first-chunk", type=int, default=6,
-                    help="rows of the short first launch that measures per-ray cost")
+    ap.add_argument("--first-chunk", default="6",
+                    help="rows of the short leading launches that measure per-ray cost (comma list)")
     ap.add_argument("--lib", default=None, help="alternative librwrt build (A/B timing)")
     ap.add_argument("--traffic", default=None,
                     help="traffic.json from tools/pmc_traffic.py (default: newest profiles/*/traffic.json "
@@ -148,7 +149,7 @@ def main():
     def one_step(events=None):
         return eng.integrate(y0_d, nt, 7200.0, ttotal=(nt - 1) * 7200.0, chunk=chunk, out=out,
                              events=events, order_policy=args.order,
-                             first_chunk=args.first_chunk)
+                             first_chunk=[int(x) for x in str(args.first_chunk).split(",") if x])
 
     for _ in range(args.warmup):
         one_step()
@@ -186,7 +187,8 @@ def main():
         achieved = per_launch_steps * BYTES_PER_STEP / avg_launch_s
         workload = (f"C3: 2deg global seeds x k=1..10 x {args.periods} periods, "
                     f"{args.days:g} d at 2 h, 2.5deg DJF jet background (BASELINE configs[2])")
-        traffic, tsrc = find_traffic(args.traffic, workload)
+        schedule = [b - a for a, b in r.bounds]
+        traffic, tsrc = find_traffic(args.traffic, workload, schedule)
         result = {
             "metric": METRIC, "value": value, "unit": "ray-steps/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
@@ -194,7 +196,8 @@ def main():
             "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
             "config": {"workload": workload,
                        "ray_slots_per_gpu": nslot, "live_rays_per_gpu": n_live, "rows": nt,
-                       "rows_per_launch": chunk, "parallelism": f"rays sharded, {world} rank(s), 1 GPU each"},
+                       "rows_per_launch": chunk, "launch_rows": [b - a for a, b in r.bounds],
+                       "parallelism": f"rays sharded, {world} rank(s), 1 GPU each"},
             "ray_steps_per_step": steps_done / args.steps,
             "rejected_per_accepted": rej / max(r.ray_steps, 1),
             "host_init_s": t_init,

@@ -155,7 +155,8 @@ rwrt_status rwrt_kat_rk45(int32_t kind, int64_t ncol, const double* d_y0,
  * routines the kernels use.  kind: 0 sin(x), 1 cos(x), 2 tan(x), 3 pow(x, y),
  * 4 atan2(x, y), 5 Python x % y (fmod-based), 6 sqrt(x), 7 x / y, 8 floor(x),
  * 9/10 sin/cos through sincos(x), 11 x / 6.3712e6 (the kernels' exact division
- * by the earth radius), 12 fmod(x, y) for y > 0 (the kernels' exact fmod).
+ * by the earth radius), 12 fmod(x, y) for y > 0 (the kernels' exact fmod),
+ * 13 x % (2 pi) and 14 (x % (2 pi)) % (2 pi) as the kernels evaluate them.
  * Lets the tests prove which operations are bit-exact on the GPU (IEEE
  * division, sqrt, fmod) and measure the last-bit agreement of the rest. */
 rwrt_status rwrt_selftest_math(int32_t kind, int64_t n, const double* d_x,

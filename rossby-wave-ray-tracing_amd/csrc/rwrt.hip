@@ -82,12 +82,15 @@ __device__ __forceinline__ double np_min(double a, double b) {
 // remainder |a| - n b is a multiple of ulp(b) below b, so one FMA computes it
 // exactly, and a wrong n shows up as a remainder outside [0, b) (a sign test,
 // which rounding cannot flip).  A third of the library routine's cost.
-__device__ __forceinline__ double fmod_pos(double a, double b) {
+// binv (optional) ~ 1/b replaces the division: its quotient is off by at most
+// one too (relative error ~2^-52 of a quotient below 2^40), which the same
+// correction absorbs.
+__device__ __forceinline__ double fmod_pos(double a, double b, double binv = 0.0) {
   const double x = fabs(a);
   if (!(x < 0x1p40)) return fmod(a, b);      // NaN, inf, huge: library routine
   double r = x;
   if (x >= b) {
-    double n = trunc(x / b);
+    double n = trunc(binv != 0.0 ? x * binv : x / b);
     r = fma(-n, b, x);
     if (r < 0.0) {
       n -= 1.0;
@@ -102,8 +105,8 @@ __device__ __forceinline__ double fmod_pos(double a, double b) {
 
 // Python/NumPy floor modulo for float64 (npy_remainder): fmod, then move a
 // remainder whose sign differs from b into [0, b); exact zero gets b's sign.
-__device__ __forceinline__ double py_mod(double a, double b) {
-  double m = fmod_pos(a, b);
+__device__ __forceinline__ double py_mod(double a, double b, double binv = 0.0) {
+  double m = fmod_pos(a, b, binv);
   if (m != 0.0) {
     if ((b < 0.0) != (m < 0.0)) m += b;
   } else {
@@ -111,6 +114,13 @@ __device__ __forceinline__ double py_mod(double a, double b) {
   }
   return m;
 }
+// x % (2 * pi) (bs.py:519, interpolation.py:80)
+constexpr double kInvTwoPi = 1.0 / kTwoPi;
+__device__ __forceinline__ double py_mod_2pi(double a) { return py_mod(a, kTwoPi, kInvTwoPi); }
+// py_mod_2pi(m) for m = py_mod_2pi(x), which lies in [0, 2 pi] or is NaN: the
+// identity, except that a remainder that rounded up to 2 pi itself becomes +0.
+__device__ __forceinline__ double py_mod_2pi_again(double m) { return (m >= kTwoPi) ? 0.0 : m; }
+
 // np.floor(x).astype('int32') on x86-64: out-of-range and NaN give INT32_MIN.
 __device__ __forceinline__ int64_t floor_i32(double x) {
   double f = floor(x);
@@ -130,6 +140,9 @@ constexpr int kNF = RWRT_NFIELD_PACK;
 // the six third derivatives are never read on the hot path.
 __constant__ int kRefIndex[11] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 11};
 
+#ifndef RWRT_STAGE_BARRIER
+#define RWRT_STAGE_BARRIER 0
+#endif
 #ifndef RWRT_INTERP_GROUP
 #define RWRT_INTERP_GROUP 6   // records (of 2 fields) per load group, divides 6
 #endif
@@ -152,7 +165,7 @@ struct Corners {
 
 __device__ __forceinline__ Corners corners(const Field& F, double lon, double lat) {
   // lon arrives already reduced once (bs.py:519); interpolation.py:80 reduces again.
-  const double lons = py_mod(lon, kTwoPi);
+  const double lons = py_mod_2pi_again(lon);
   const double x = (lons - F.lon0) / F.dlon;
   const double y = (lat - F.lat0) / F.dlat;
   const int64_t ix = floor_i32(x), iy = floor_i32(y);
@@ -271,16 +284,22 @@ __device__ __forceinline__ void ugvg(double fu, double fv, double fqx, double fq
 // ---------------------------------------------------------------------------
 // The RHS: WR.diffun_numpy (wr.py:492-556) + core_diffun (wr.py:44-82)
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void ray_rhs(const Field& F, const double* y, double* dy) {
+//
+// aux (optional) receives {ug, vg, cos(lat)} of this evaluation -- exactly what
+// the per-interval post-processing recomputes at the same position
+// (wr.py:844, 856-865) -- or NaN for a masked ray (no values computed).
+__device__ __forceinline__ void ray_rhs(const Field& F, const double* y, double* dy,
+                                        double* aux = nullptr) {
   const double lon = y[0], lat = y[1], kx = y[2], ky = y[3], amp = y[4];
   // wr.py:508-514 -- a masked ray returns NaN for every derivative (wr.py:552-553)
   if (fabs(lat) >= kHalfPi || fabs(ky) >= 100.0) {
 #pragma unroll
     for (int v = 0; v < 5; ++v) dy[v] = kNaN;
+    if (aux) aux[0] = aux[1] = aux[2] = kNaN;
     return;
   }
   double g[11];
-  interp11(F, py_mod(lon, kTwoPi), lat, g);
+  interp11(F, py_mod_2pi(lon), lat, g);
   double s, c;
   sincos(lat, &s, &c);              // one argument reduction for both (== sin(), cos())
   const double tn = tan(lat);
@@ -307,13 +326,18 @@ __device__ __forceinline__ void ray_rhs(const Field& F, const double* y, double*
   dy[2] = div_rearth(dzwn);
   dy[3] = div_rearth(dmwn);
   dy[4] = div_rearth(damp * amp);
+  if (aux) {
+    aux[0] = ug;
+    aux[1] = vg;
+    aux[2] = c;
+  }
 }
 
 // group velocity at a stored position (wr.py:856-865): no |l| mask here
 __device__ __forceinline__ void ugvg_at(const Field& F, double lon, double lat, double k,
                                         double l, double& ug, double& vg) {
   double fu, fv, fqx, fqy;
-  interp4(F, py_mod(lon, kTwoPi), lat, fu, fv, fqx, fqy);
+  interp4(F, py_mod_2pi(lon), lat, fu, fv, fqx, fqy);
   const double c = cos(lat);
   const double m = (fabs(c) <= 0.0175) ? 0.0 : 1.0;
   const double cp = c * m + (1.0 - m) * 1e-6;
@@ -327,36 +351,51 @@ __device__ __forceinline__ double cal_dis(double lon_c, double lat_c, double lon
   const double a = sd * sd + (cos(lat_p) * cos(lat_c)) * (sl * sl);
   return fabs(2.0 * atan2(sqrt(a), sqrt(1.0 - a)));
 }
+// the same with cos(lat_p), cos(lat_c) supplied by the caller
+__device__ __forceinline__ double cal_dis_c(double lon_c, double lat_c, double lon_p, double lat_p,
+                                            double cos_c, double cos_p) {
+  const double sd = sin((lat_c - lat_p) / 2.0);
+  const double sl = sin((lon_c - lon_p) / 2.0);
+  const double a = sd * sd + (cos_p * cos_c) * (sl * sl);
+  return fabs(2.0 * atan2(sqrt(a), sqrt(1.0 - a)));
+}
 
 // ---------------------------------------------------------------------------
 // Problems the stepper integrates
 // ---------------------------------------------------------------------------
 struct RayProblem {
   static constexpr int NV = 5;
+  static constexpr int NAUX = 3;             // ug, vg, cos(lat) of the evaluation
   static constexpr bool kAutonomous = true;  // fun ignores t (wr.py:784-789)
   Field F;
-  __device__ __forceinline__ void operator()(double, const double* y, double* dy) const {
-    ray_rhs(F, y, dy);
+  __device__ __forceinline__ void operator()(double, const double* y, double* dy,
+                                             double* aux = nullptr) const {
+    ray_rhs(F, y, dy, aux);
   }
 };
 
 // rkf45.py demo ODEs (rkf45.py:775-782, 839-841, 861-863)
 struct KatLinear {
   static constexpr int NV = 1;
+  static constexpr int NAUX = 0;
   static constexpr bool kAutonomous = false;
-  __device__ void operator()(double t, const double* y, double* dy) const { dy[0] = 2.0 * t + y[0] * 0.0; }
+  __device__ void operator()(double t, const double* y, double* dy, double* = nullptr) const {
+    dy[0] = 2.0 * t + y[0] * 0.0;
+  }
 };
 struct KatExp {
   static constexpr int NV = 1;
+  static constexpr int NAUX = 0;
   static constexpr bool kAutonomous = false;
-  __device__ void operator()(double t, const double* y, double* dy) const {
+  __device__ void operator()(double t, const double* y, double* dy, double* = nullptr) const {
     dy[0] = pow(2.718281828459045, 0.1 * t) + y[0] * 0.0;  // np.e ** (0.1 * t)
   }
 };
 struct KatLorenz {
   static constexpr int NV = 3;
+  static constexpr int NAUX = 0;
   static constexpr bool kAutonomous = false;
-  __device__ void operator()(double, const double* u, double* d) const {
+  __device__ void operator()(double, const double* u, double* d, double* = nullptr) const {
     const double p = 10.0, b = 8.0 / 3, r = 28.0;
     const double x = u[0], y = u[1], z = u[2];
     d[0] = (-p) * x + p * y;
@@ -370,7 +409,9 @@ struct KatLorenz {
 // ---------------------------------------------------------------------------
 // Stage weights: row s = 1..5 is A[s][0..4] (stage inputs), row 6 is B[0..5]
 // (y_new); the time offset of stage 6 is c = 1 (K6 = fun(t + h, y_new)).
-__constant__ double kW[7][6] = {
+// Only ever indexed by compile-time stage numbers (stage_input<S>), so the
+// weights are instruction immediates, not loads.
+constexpr double kW[7][6] = {
     {0, 0, 0, 0, 0, 0},
     {kA[1][0], 0, 0, 0, 0, 0},
     {kA[2][0], kA[2][1], 0, 0, 0, 0},
@@ -378,15 +419,14 @@ __constant__ double kW[7][6] = {
     {kA[4][0], kA[4][1], kA[4][2], kA[4][3], 0, 0},
     {kA[5][0], kA[5][1], kA[5][2], kA[5][3], kA[5][4], 0},
     {kB[0], kB[1], kB[2], kB[3], kB[4], kB[5]}};
-__constant__ double kCs[7] = {0.0, kC[1], kC[2], kC[3], kC[4], kC[5], 1.0};
+constexpr double kCs[7] = {0.0, kC[1], kC[2], kC[3], kC[4], kC[5], 1.0};
 
-// Storage of the stages K0..K5 of one attempt, per lane: in registers, or in a
-// per-thread slice of LDS (frees 60 VGPRs of the ray kernel for occupancy).
+// Storage of the stages K1..K5 of one attempt, per lane: in registers, or in a
+// per-thread slice of LDS (frees 50 VGPRs of the ray kernel for occupancy).
 template <int NV>
 struct KRegs {
   double k[6][NV];
   __device__ __forceinline__ double get(int j, int v) const { return k[j][v]; }
-  __device__ __forceinline__ void put(int j, int v, double x) { k[j][v] = x; }
   // stage index s is wave-uniform; select the register row statically
   __device__ __forceinline__ void put_stage(int s, const double* r) {
 #pragma unroll
@@ -398,62 +438,82 @@ struct KRegs {
   }
 };
 
+// K1..K5 only (K0 is the step's f, in registers).
 template <int NV>
 struct KShared {
-  double* p;   // this lane's slice: element (j, v) at p[(j * NV + v) * stride]
+  double* p;   // this lane's slice: element (j, v) at p[((j - 1) * NV + v) * stride]
   int stride;  // threads per block
-  __device__ __forceinline__ double get(int j, int v) const { return p[(j * NV + v) * stride]; }
-  __device__ __forceinline__ void put(int j, int v, double x) { p[(j * NV + v) * stride] = x; }
+  __device__ __forceinline__ double get(int j, int v) const { return p[((j - 1) * NV + v) * stride]; }
   __device__ __forceinline__ void put_stage(int s, const double* r) {
 #pragma unroll
-    for (int v = 0; v < NV; ++v) p[(s * NV + v) * stride] = r[v];
+    for (int v = 0; v < NV; ++v) p[((s - 1) * NV + v) * stride] = r[v];
   }
 };
 
-// np.einsum('snf,s->nf', K[:s], w) in NumPy's order, s <= 6 wave-uniform:
-// sequential in j for more than one variable; for one variable einsum's
-// 2-lane SIMD dot product sums even and odd terms separately
-// (oracle/rwrt_oracle.py wsum).
-template <int NV, class KS>
-__device__ __forceinline__ double wsum(const KS& K, const double* w, int s, int v) {
+// np.einsum('snf,s->nf', K[:S], w) in NumPy's order for stage S: sequential
+// in j for more than one variable; for one variable einsum's 2-lane SIMD dot
+// product sums even and odd terms separately (oracle/rwrt_oracle.py wsum).
+// K0 is the step's f (registers); K1..K5 come from KS.  Zero weights (B[1])
+// are kept: NumPy multiplies them too (NaN/inf propagate).
+template <int S, int NV, class KS>
+__device__ __forceinline__ double wsum(const KS& K, const double* f, int v) {
   if constexpr (NV == 1) {
     double even = 0.0, odd = 0.0;
 #pragma unroll
-    for (int j = 0; j < 6; ++j) {
-      if (j < s) {
-        if (j % 2 == 0) even = even + K.get(j, v) * w[j];
-        else odd = odd + K.get(j, v) * w[j];
-      }
+    for (int j = 0; j < S; ++j) {
+      const double kj = (j == 0) ? f[v] : K.get(j, v);
+      if (j % 2 == 0) even = even + kj * kW[S][j];
+      else odd = odd + kj * kW[S][j];
     }
     return even + odd;
   } else {
     double acc = 0.0;
 #pragma unroll
-    for (int j = 0; j < 6; ++j)
-      if (j < s) acc = acc + K.get(j, v) * w[j];
+    for (int j = 0; j < S; ++j) acc = acc + ((j == 0) ? f[v] : K.get(j, v)) * kW[S][j];
     return acc;
   }
+}
+
+// Input (t_s, y_s) of stage S (rkf45.py:300-306).
+template <int S, int NV, class KS>
+__device__ __forceinline__ double stage_input(const KS& K, double t, const double* y,
+                                              const double* f, double h, double* ys) {
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    ys[v] = y[v] + wsum<S, NV>(K, f, v) * h;
+#if RWRT_STAGE_BARRIER
+    __builtin_amdgcn_sched_barrier(0);   // bound the LDS reads in flight (registers)
+#endif
+  }
+  return t + kCs[S] * h;
 }
 
 // One DP5(4) attempt: rk_step (rkf45.py:259-321) + _estimate_error_norm
 // (rkf45.py:368-373).  The six stage evaluations share ONE inlined copy of the
 // RHS (a wave-uniform stage loop), which keeps the kernel's code small and its
 // register file for occupancy.  Returns the error norm (NaN kept); fills y_new,
-// K6 and, if Kout is given, all seven stages.
+// K6, if aux is given the problem's side outputs of the K6 evaluation (at
+// y_new), and if Kout is given all seven stages.
 template <class P, class KS>
 __device__ __forceinline__ double dp54_attempt(const P& fun, KS& K, double t, const double* y,
                                                const double* f, double h, double rtol,
                                                double atol, double* ynew, double* k6,
-                                               double* Kout = nullptr, int64_t kstride = 0) {
+                                               double* Kout = nullptr, int64_t kstride = 0,
+                                               double* aux = nullptr) {
   constexpr int NV = P::NV;
-#pragma unroll
-  for (int v = 0; v < NV; ++v) K.put(0, v, f[v]);
   double ys[NV], r[NV];
 #pragma nounroll
   for (int s = 1; s <= 6; ++s) {
-#pragma unroll
-    for (int v = 0; v < NV; ++v) ys[v] = y[v] + wsum<NV>(K, kW[s], s, v) * h;
-    fun(t + kCs[s] * h, ys, r);
+    double ts;
+    switch (s) {   // wave-uniform: one straight-line combination per stage
+      case 1: ts = stage_input<1, NV>(K, t, y, f, h, ys); break;
+      case 2: ts = stage_input<2, NV>(K, t, y, f, h, ys); break;
+      case 3: ts = stage_input<3, NV>(K, t, y, f, h, ys); break;
+      case 4: ts = stage_input<4, NV>(K, t, y, f, h, ys); break;
+      case 5: ts = stage_input<5, NV>(K, t, y, f, h, ys); break;
+      default: ts = stage_input<6, NV>(K, t, y, f, h, ys); break;
+    }
+    fun(ts, ys, r, aux);
     if (s < 6) K.put_stage(s, r);
   }
   // after the loop: ys = y + h*(B . K[:6]) = y_new, r = K6
@@ -467,15 +527,16 @@ __device__ __forceinline__ double dp54_attempt(const P& fun, KS& K, double t, co
       double even = 0.0, odd = 0.0;
 #pragma unroll
       for (int j = 0; j < 6; ++j) {
-        if (j % 2 == 0) even = even + K.get(j, v) * kE[j];
-        else odd = odd + K.get(j, v) * kE[j];
+        const double kj = (j == 0) ? f[v] : K.get(j, v);
+        if (j % 2 == 0) even = even + kj * kE[j];
+        else odd = odd + kj * kE[j];
       }
       even = even + r[v] * kE[6];
       es = even + odd;
     } else {
       es = 0.0;
 #pragma unroll
-      for (int j = 0; j < 6; ++j) es = es + K.get(j, v) * kE[j];
+      for (int j = 0; j < 6; ++j) es = es + ((j == 0) ? f[v] : K.get(j, v)) * kE[j];
       es = es + r[v] * kE[6];
     }
     const double e = h * es;
@@ -487,7 +548,7 @@ __device__ __forceinline__ double dp54_attempt(const P& fun, KS& K, double t, co
 #pragma unroll
     for (int j = 0; j < 6; ++j)
 #pragma unroll
-      for (int v = 0; v < NV; ++v) Kout[(j * NV + v) * kstride] = K.get(j, v);
+      for (int v = 0; v < NV; ++v) Kout[(j * NV + v) * kstride] = (j == 0) ? f[v] : K.get(j, v);
 #pragma unroll
     for (int v = 0; v < NV; ++v) Kout[(6 * NV + v) * kstride] = r[v];
   }
@@ -540,6 +601,9 @@ struct Lane {
   static constexpr int NV = P::NV;
   KS K;
   double y[NV], f[NV];
+  // side outputs of the last evaluation at y (valid after an accepted step;
+  // the caller sets aux[NAUX-1] = NaN whenever y changes otherwise)
+  double aux[P::NAUX > 0 ? P::NAUX : 1];
   double t, habs, hs;
   bool in_step, rejected;
 
@@ -569,7 +633,8 @@ struct Lane {
     h = tn - t;
     const double ha = fabs(h);
     double yn[NV], k6[NV];
-    double en = dp54_attempt(fun, K, t, y, f, h, rtol, atol, yn, k6);
+    double en = dp54_attempt(fun, K, t, y, f, h, rtol, atol, yn, k6, nullptr, 0,
+                             P::NAUX > 0 ? aux : nullptr);
     if (en != en) en = 0.0;                 // rkf45.py:446
     if (en < 1.0) {
       double fac = np_min(kMaxFactor, kSafety * pow(en, kErrExp));
@@ -613,7 +678,7 @@ __global__ void mercator_kernel(Field F, int64_t n, const double* __restrict__ l
        i += (int64_t)gridDim.x * blockDim.x) {
     const double la = lat[i];
     double g[11], o[12];
-    interp11(F, py_mod(lon[i], kTwoPi), la, g);
+    interp11(F, py_mod_2pi(lon[i]), la, g);
     const Merc M = merc_factors(la, cos(la), sin(la));
     mercator12(g, M, tan(la), o);
 #pragma unroll
@@ -736,7 +801,7 @@ __global__ void __launch_bounds__(256, RWRT_WAVES_PER_SIMD) rk45_run_kernel(RunA
   const RayProblem P{a.F};
   const int64_t nrows = a.it_end - a.it_begin;
 #if RWRT_K_IN_LDS
-  __shared__ double kbuf[6 * 5 * 256];
+  __shared__ double kbuf[5 * 5 * 256];
   Lane<RayProblem, KStore> L;
   L.K.p = kbuf + threadIdx.x;
   L.K.stride = 256;
@@ -745,7 +810,7 @@ __global__ void __launch_bounds__(256, RWRT_WAVES_PER_SIMD) rk45_run_kernel(RunA
 #endif
   int64_t ray = -1, nacc = 0, nrej = 0;
   int32_t it = 0, nanrow = 0;
-  double prev_lon = 0.0, prev_lat = 0.0;
+  double prev_lon = 0.0, prev_lat = 0.0, cos_prev = 0.0;
   const bool heavy = (int)blockIdx.x < a.heavy_blocks;
   bool heavy_left = heavy && a.n_heavy > 0;
   if (heavy) __builtin_amdgcn_s_setprio(3);
@@ -780,23 +845,38 @@ __global__ void __launch_bounds__(256, RWRT_WAVES_PER_SIMD) rk45_run_kernel(RunA
       it = a.it_begin;
       prev_lon = L.y[0];   // == rlon[it-1], rlat[it-1] (wr.py:844, 877-885)
       prev_lat = L.y[1];
+      cos_prev = cos(prev_lat);
+      L.aux[2] = kNaN;     // no evaluation at y yet
     }
     const double tb = a.tbound[it];
     const int st = L.iterate(P, tb, a.min_step, a.rtol, a.atol, nacc, nrej);
     if (st == Lane<RayProblem, KStore>::kStep) continue;
 
     // ---- interval it reached: post-processing (wr.py:835-885) ----
+    // The last accepted step's K6 evaluation was at this y: its cos(lat), ug
+    // and vg are the values wr.py:844 and wr.py:856-865 recompute (same
+    // inputs, same operations), so they are reused unless that evaluation was
+    // masked (aux NaN) or y has changed since.
     double* y = L.y;
-    if (fabs(y[1]) >= kHalfPi) {
+    const bool have = !isnan(L.aux[2]);
+    double ug, vg, cos_c = kNaN;
+    bool masked = fabs(y[1]) >= kHalfPi;
+    if (!masked) {
+      cos_c = have ? L.aux[2] : cos(y[1]);
+      masked = cal_dis_c(y[0], y[1], prev_lon, prev_lat, cos_c, cos_prev) >= a.cut_off;
+    }
+    if (masked) {
 #pragma unroll
       for (int v = 0; v < 5; ++v) y[v] = kNaN;
+      ug = vg = kNaN;             // ugvg of a NaN position
+      cos_c = kNaN;
+      L.aux[2] = kNaN;
+    } else if (have) {
+      ug = L.aux[0];
+      vg = L.aux[1];
+    } else {
+      ugvg_at(a.F, y[0], y[1], y[2], y[3], ug, vg);
     }
-    if (cal_dis(y[0], y[1], prev_lon, prev_lat) >= a.cut_off) {
-#pragma unroll
-      for (int v = 0; v < 5; ++v) y[v] = kNaN;
-    }
-    double ug, vg;
-    ugvg_at(a.F, y[0], y[1], y[2], y[3], ug, vg);
     const double2 r0 = make_double2(y[0], y[1]), r1 = make_double2(y[2], y[3]);
     const double2 r2 = make_double2(y[4], ug), r3 = make_double2(vg, (double)nacc);
     // A frozen ray never changes again (its mean stays NaN; re-applying the
@@ -813,6 +893,7 @@ __global__ void __launch_bounds__(256, RWRT_WAVES_PER_SIMD) rk45_run_kernel(RunA
     if (nanrow == a.nt && isnan(y[0])) nanrow = it;  // wr.py:853-855 (host reduces)
     prev_lon = y[0];
     prev_lat = y[1];
+    cos_prev = cos_c;
     it = last;
     if (st == Lane<RayProblem, KStore>::kFrozen) L.t = a.tbound[a.it_end - 1];
     if (it == a.it_end) {
@@ -850,6 +931,8 @@ __global__ void math_kernel(int kind, int64_t n, const double* __restrict__ x,
     case 9: { double sn, cs; sincos(a, &sn, &cs); r = sn; } break;
     case 10: { double sn, cs; sincos(a, &sn, &cs); r = cs; } break;
     case 11: r = div_rearth(a); break;
+    case 13: r = py_mod_2pi(a); break;
+    case 14: r = py_mod_2pi_again(py_mod_2pi(a)); break;
     default: r = fmod_pos(a, b); break;
   }
   out[i] = r;
@@ -1199,7 +1282,7 @@ rwrt_status rwrt_kat_rk45(int32_t kind, int64_t ncol, const double* d_y0, int32_
 
 rwrt_status rwrt_selftest_math(int32_t kind, int64_t n, const double* d_x, const double* d_y,
                                double* d_out, void* stream) {
-  if (n < 0 || kind < 0 || kind > 12 || (n > 0 && (!d_x || !d_out)))
+  if (n < 0 || kind < 0 || kind > 14 || (n > 0 && (!d_x || !d_out)))
     return fail(RWRT_ERR_ARG, "bad selftest arguments%s");
   if (n == 0) return RWRT_OK;
   hipLaunchKernelGGL(math_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, kind,

@@ -39,6 +39,7 @@ class RunResult:
         self.failed = failed        # rkf45.py:423-425 -> wr.py:886-887
         self.break_row = break_row  # wr.py:853-855 global early exit (None = no break)
         self.n_live = n_live
+        self.bounds = []            # the [it_begin, it_end) row windows launched
 
     @property
     def ray_steps(self):
@@ -215,7 +216,8 @@ class RayEngine:
 
         ``sink(i0, i1, rows)`` receives each time chunk as a device tensor
         ``rows[nray, i1-i0, 8]`` (lon lat k l amp ug vg nacc) before the next
-        chunk overwrites it.  ``events`` (a list) collects a pair of timing
+        chunk overwrites it.  ``first_chunk`` (int or list) sets short leading
+        chunks whose measured per-ray work orders the next one.  ``events`` (a list) collects a pair of timing
         events around every ray-loop launch.  With a process ``group`` (rays
         sharded over ranks, shard.py) the two global outcomes -- solver
         failure and the all-NaN early exit -- are decided over every rank, so a
@@ -241,9 +243,13 @@ class RayEngine:
         chunk = chunk or (nt - 1)
         bounds = []
         i0 = 1
-        if first_chunk and order_policy in ("cost", "priority") and first_chunk < chunk:
-            bounds.append((1, min(1 + first_chunk, nt)))    # a short chunk to measure ray costs
-            i0 = bounds[-1][1]
+        # short leading chunks measure the per-ray cost that orders the next one
+        lead = [first_chunk] if isinstance(first_chunk, int) else list(first_chunk or [])
+        if order_policy in ("cost", "priority"):
+            for n in lead:
+                if 0 < n < chunk and i0 < nt:
+                    bounds.append((i0, min(i0 + n, nt)))
+                    i0 = bounds[-1][1]
         while i0 < nt:
             bounds.append((i0, min(i0 + chunk, nt)))
             i0 = bounds[-1][1]
@@ -275,7 +281,9 @@ class RayEngine:
             from shard import reduce_max
             mx = reduce_max(mx, group)
         brk = mx if mx < nt else None
-        return RunResult(cnt[:, 0], cnt[:, 1], st["nanrow"], False, brk, n_live)
+        res = RunResult(cnt[:, 0], cnt[:, 1], st["nanrow"], False, brk, n_live)
+        res.bounds = bounds
+        return res
 
 
 def ctypes_ref(p):
@@ -298,7 +306,7 @@ def kat_rk45(kind, y0, t_eval, rtol, atol, min_step, device="cuda"):
 
 MATH_KINDS = {"sin": 0, "cos": 1, "tan": 2, "pow": 3, "atan2": 4, "mod": 5, "sqrt": 6,
               "div": 7, "floor": 8, "sincos_sin": 9, "sincos_cos": 10, "div_rearth": 11,
-              "fmod": 12}
+              "fmod": 12, "mod2pi": 13, "mod2pi_twice": 14}
 
 
 def selftest_math(name, x, y=None, device="cuda"):

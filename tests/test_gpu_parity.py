@@ -312,6 +312,13 @@ def test_device_math_exactness():
     with np.errstate(all="ignore"):
         assert np.array_equal(selftest_math("fmod", near, np.full(near.shape, tp)),
                               np.fmod(near, tp), equal_nan=True)
+    # the kernels' x % (2 pi) (reciprocal quotient) and the second reduction
+    # of interpolation.py:80 (a clamp) equal NumPy's
+    wrap = np.concatenate([lon, near[np.isfinite(near)], -near[np.isfinite(near)],
+                           np.nextafter(-0.0, -1) * np.arange(1, 50), [np.inf, np.nan]])
+    with np.errstate(all="ignore"):
+        assert np.array_equal(selftest_math("mod2pi", wrap), wrap % tp, equal_nan=True)
+        assert np.array_equal(selftest_math("mod2pi_twice", wrap), (wrap % tp) % tp, equal_nan=True)
     rates = {}
     for name in ("sin", "cos", "tan"):
         rates[name] = float(np.mean(selftest_math(name, lat) != getattr(np, name)(lat)))

@@ -32,7 +32,8 @@ def main():
     n = min(len(f), len(w))
     fb, wb = sum(f[:n]) / n, sum(w[:n]) / n
     steps_per_launch = bench["ray_steps_per_step"] / (bench["roofline"]["launches"] / bench["steps"])
-    res = {"workload": bench["config"]["workload"], "kernel": "rk45_run_kernel", "launches": n,
+    res = {"workload": bench["config"]["workload"], "launch_rows": bench["config"].get("launch_rows"),
+           "kernel": "rk45_run_kernel", "launches": n,
            "fetch_bytes_per_launch_x2": 2 * fb, "write_bytes_per_launch": wb,
            "traffic_bytes_per_launch": 2 * fb + wb,
            "algorithmic_bytes_per_launch": steps_per_launch * bench["roofline"]["bytes_per_ray_step"],
