@@ -108,7 +108,7 @@ def main():
     ap.add_argument("--order", default="priority", choices=["priority", "cost", "live"],
                     help="work-queue order: heaviest rays to high-priority waves (priority), "
                          "longest-first (cost), or live-first")
-    ap.add_argument("--first-chunk", default="6",
+    ap.add_argument("--first-chunk", default="6,24,96",
                     help="rows of the short leading launches that measure per-ray cost (comma list)")
     ap.add_argument("--lib", default=None, help="alternative librwrt build (A/B timing)")
     ap.add_argument("--traffic", default=None,
@@ -143,7 +143,10 @@ def main():
     eng = RayEngine.from_bs(bs, device=dev)
     y0_d = torch.as_tensor(y0, device=dev)
     nt = int(round(args.days * 12)) + 1
-    chunk = args.chunk or max(1, min(nt - 1, (8 << 30) // (nslot * 64)))
+    # the whole history stays in HBM when it fits (C3: 166 GB of 288 GB), so
+    # the ray loop is a few launches: short cost probes, then all the rest
+    free = torch.cuda.mem_get_info(dev)[0]
+    chunk = args.chunk or max(1, min(nt - 1, int(0.8 * free) // (nslot * 64)))
     out = torch.empty((nslot, min(chunk, nt - 1), 8), dtype=torch.float64, device=dev)
 
     def one_step(events=None):
