@@ -82,7 +82,7 @@ def find_traffic(path, workload, schedule):
     """Per-launch HBM bytes of the ray kernel from a PMC profile of this workload
     run with the same launch schedule (rows per launch)."""
     import glob
-    cands = [path] if path else sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "traffic.json")),
+    cands = [path] if path else sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "traffic.json"), recursive=True),
                                        key=os.path.getmtime, reverse=True)
     for c in cands:
         try:
