@@ -53,6 +53,17 @@ def c3_initial_state(bs, lon_offset_deg=0.0, periods=S.C3_PERIODS_DAYS):
     return np.concatenate(ys, axis=1)
 
 
+def c3_sources(eng, lon_offset_deg=0.0, periods=S.C3_PERIODS_DAYS):
+    """Device inputs of the GPU initialiser for C3: the source list and one
+    per-k constant block per period."""
+    cfg = S.config("C3")
+    deg2rad = np.pi / 180.0
+    ix, iy = np.meshgrid(np.arange(cfg.nnx), np.arange(cfg.nny))
+    lon = (((cfg.SW_lon + lon_offset_deg) % 360.0 + ix.ravel() * cfg.dlon) % 360.0) * deg2rad
+    lat = (cfg.SW_lat + iy.ravel() * cfg.dlat) * deg2rad
+    return eng.sources(lon, lat), [eng.zwn_tensor(cfg.zwn, S.c3_freq(P)) for P in periods]
+
+
 def make_bs(kind="zonal"):
     from bs import BS
     bg = S.background(kind)
@@ -110,6 +121,8 @@ def main():
                          "longest-first (cost), or live-first")
     ap.add_argument("--first-chunk", default="6,24,96",
                     help="rows of the short leading launches that measure per-ray cost (comma list)")
+    ap.add_argument("--init", default="gpu", choices=["gpu", "host"],
+                    help="initial rows: GPU kernel inside each step (default) or host rows resident")
     ap.add_argument("--lib", default=None, help="alternative librwrt build (A/B timing)")
     ap.add_argument("--traffic", default=None,
                     help="traffic.json from tools/pmc_traffic.py (default: newest profiles/*/traffic.json "
@@ -132,17 +145,36 @@ def main():
 
     from engine import RayEngine
     bs, bg = make_bs("zonal")
+    periods = S.C3_PERIODS_DAYS[: args.periods]
+    lon_off = rank * 2.0 / max(world, 1)
     t_init = time.perf_counter()
-    y0 = c3_initial_state(bs, lon_offset_deg=rank * 2.0 / max(world, 1),
-                          periods=S.C3_PERIODS_DAYS[: args.periods])
+    y0 = c3_initial_state(bs, lon_offset_deg=lon_off, periods=periods)
     t_init = time.perf_counter() - t_init
     if args.replicate > 1:
         y0 = np.concatenate([y0] * args.replicate, axis=1)
     nslot = y0.shape[1]
     n_live = int(np.sum(~np.isnan(y0.mean(axis=0))))
     eng = RayEngine.from_bs(bs, device=dev)
-    y0_d = torch.as_tensor(y0, device=dev)
     nt = int(round(args.days * 12)) + 1
+    gpu_init = args.init == "gpu" and args.replicate == 1
+    if gpu_init:
+        # sources and per-k constants resident in HBM; the step starts from them
+        src, zcs = c3_sources(eng, lon_off, periods)
+        init_rows = [None] * len(zcs)
+        init_info = torch.zeros(1, dtype=torch.int32, device=dev)
+
+        def make_y0():
+            ys = []
+            for j, zc in enumerate(zcs):
+                init_rows[j], _ = eng.initial_rows_dev(src, zc, init_rows[j], init_info)
+                ys.append(init_rows[j][:5].reshape(5, -1))
+            return torch.cat(ys, dim=1)
+        y0_d = make_y0()
+        hy = torch.as_tensor(y0)
+        init_same = bool(((y0_d.cpu() == hy) | (torch.isnan(y0_d.cpu()) & torch.isnan(hy))).all())
+    else:
+        init_same = None
+        y0_d = torch.as_tensor(y0, device=dev)
     # the whole history stays in HBM when it fits (C3: 166 GB of 288 GB), so
     # the ray loop is a few launches: short cost probes, then all the rest
     free = torch.cuda.mem_get_info(dev)[0]
@@ -150,7 +182,8 @@ def main():
     out = torch.empty((nslot, min(chunk, nt - 1), 8), dtype=torch.float64, device=dev)
 
     def one_step(events=None):
-        return eng.integrate(y0_d, nt, 7200.0, ttotal=(nt - 1) * 7200.0, chunk=chunk, out=out,
+        y = make_y0() if gpu_init else y0_d
+        return eng.integrate(y, nt, 7200.0, ttotal=(nt - 1) * 7200.0, chunk=chunk, out=out,
                              events=events, order_policy=args.order,
                              first_chunk=[int(x) for x in str(args.first_chunk).split(",") if x])
 
@@ -204,6 +237,9 @@ def main():
             "ray_steps_per_step": steps_done / args.steps,
             "rejected_per_accepted": rej / max(r.ray_steps, 1),
             "host_init_s": t_init,
+            "init": ("GPU rwrt_ray_initial inside every timed step (bit-identical to the host rows)"
+                     if gpu_init else "host NumPy rows, outside the timed region"),
+            "init_bitwise_vs_host": init_same,
             "queue_order": args.order,
             "library": os.path.basename(os.environ.get("RWRT_LIB", "librwrt.so")),
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,

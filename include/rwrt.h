@@ -94,6 +94,29 @@ rwrt_status rwrt_dp54_attempt(const rwrt_grid* g, const double* d_packed,
                               double* d_K, double* d_ynew, double* d_err,
                               void* stream);
 
+/* Initial rays WR.ray_initial_numpy (wr.py:344-395) on the device, per
+ * (source, zonal wavenumber): the Mercator point at the source
+ * (cal_bs_mercator_point, bs.py:781-887), the meridional wavenumbers of the
+ * t = 0 dispersion relation (cal_ky_numpy, bs.py:985-1040 -- np.roots
+ * restated operation for operation: companion matrix, LAPACK zgeev's
+ * zgebal + zlahqr, csrc/nproots.h), change_roots_order (bs.py:942-982) and
+ * the t = 0 group velocity (cal_ugvg_numpy, wn.py:209-259).
+ *  d_src_lon, d_src_lat, d_src_cos [nsource]: source position (radians, as
+ *    set_source_matrix makes it, wr.py:236-258) and np.cos(lat) from the
+ *    host libm -- the one transcendental of this path, so that it is the
+ *    reference's own value.
+ *  d_zwn[4][nzwn] = {k, k**2, k**3, freq / k * R} as NumPy evaluates them
+ *    (bs.py:1005-1012).
+ *  d_rows[7][3][nsource][nzwn] = lon lat k l amp ug vg (wr.py:160-167
+ *    layout of row 0; NaN where a slot has no real root).
+ *  d_info[1] (int32, zeroed by this call) counts polynomials with
+ *    non-finite coefficients -- np.linalg.eigvals raises LinAlgError there;
+ *    the host raises too when it is non-zero. */
+rwrt_status rwrt_ray_initial(const rwrt_grid* g, const double* d_packed,
+                             int64_t nsource, const double* d_src_lon,
+                             const double* d_src_lat, const double* d_src_cos,
+                             int32_t nzwn, const double* d_zwn, double* d_rows,
+                             int32_t* d_info, void* stream);
 /* Solver construction: RungeKutta.__init__ (rkf45.py:335-366) with
  * select_initial_step (rkf45.py:34-99) on d_y0[5][nray].
  * Writes d_state[12][nray] = y f t(=0) h_abs, zeroes d_count[nray][2]

@@ -15,8 +15,8 @@ LIB_PATH = os.environ.get("RWRT_LIB", os.path.join(_HERE, "librwrt.so"))
 NFIELD_REF, NFIELD_PACK, NVAR, NMERC, NOUT, NSTATE = 18, 12, 5, 12, 8, 12
 ABI_SYMBOLS = ("rwrt_version", "rwrt_last_error", "rwrt_pack_fields",
                "rwrt_mercator_point", "rwrt_rhs", "rwrt_dp54_attempt",
-               "rwrt_rk45_init", "rwrt_rk45_run", "rwrt_rk4_run", "rwrt_kat_rk45",
-               "rwrt_selftest_math")
+               "rwrt_ray_initial", "rwrt_rk45_init", "rwrt_rk45_run", "rwrt_rk4_run",
+               "rwrt_kat_rk45", "rwrt_selftest_math")
 
 RWRT_OK, RWRT_ERR_ARG, RWRT_ERR_HIP, RWRT_SOLVER_FAILED = 0, 1, 2, 3
 
@@ -66,6 +66,7 @@ def load():
         "rwrt_mercator_point": [G, _P, _I64, _P, _P, _P, _P],
         "rwrt_rhs": [G, _P, _I64, _P, _P, _P],
         "rwrt_dp54_attempt": [G, _P, _I64, _P, _P, _P, _D, _D, _P, _P, _P, _P],
+        "rwrt_ray_initial": [G, _P, _I64, _P, _P, _P, _I32, _P, _P, _P, _P],
         "rwrt_rk45_init": [G, _P, _I64, _P, Pr, _P, _P, _P, _P, _P, _P],
         "rwrt_rk45_run": [G, _P, _I64, Pr, _P, _I32, _I32, _P, _I64, _P, _P, _P, _P, _P, _P],
         "rwrt_rk4_run": [G, _P, _I64, Pr, _I32, _I32, _P, _P, _P, _P, _P, _P, _P],

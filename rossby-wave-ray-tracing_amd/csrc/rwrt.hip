@@ -21,6 +21,7 @@
 #include <string>
 
 #include "rwrt.h"
+#include "nproots.h"
 
 namespace rwrt {
 
@@ -1062,6 +1063,103 @@ __global__ void kat_kernel(int64_t ncol, const double* __restrict__ y0, int32_t 
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// Initial rays: WR.ray_initial_numpy (wr.py:344-395)
+// ---------------------------------------------------------------------------
+// change_roots_order (bs.py:942-982) on the nreal compacted real roots, then
+// the |m| > 100 filter and the reversal of cal_ky (bs.py:1037-1040).
+__device__ __forceinline__ void order_roots(double m[3], int nreal) {
+  auto swap = [&](int a, int b) { const double t = m[a]; m[a] = m[b]; m[b] = t; };
+  if (nreal == 3) {
+    if (m[2] >= 0.0 && m[2] < m[1]) swap(1, 2);
+    if (m[0] < 0.0) swap(0, 1);
+    if ((m[1] < 0.0 && m[2] < 0.0 && m[1] < m[2]) || (m[1] > 0.0 && m[2] < 0.0)) swap(1, 2);
+  } else if (nreal == 2) {
+    if (!(m[0] > 0.0)) swap(0, 1);
+  } else if (nreal == 1) {
+    if (m[0] < 0.0) swap(0, 1);
+  }
+#pragma unroll
+  for (int q = 0; q < 3; ++q)
+    if (!isnan(m[q]) && fabs(m[q]) > 100.0) m[q] = kNaN;
+  swap(0, 2);
+}
+
+// One thread per (source, zonal wavenumber).  zc = {k, k**2, k**3, freq/k*R}
+// for every k (NumPy-evaluated on the host); rows[7][3][nsource][nzwn].
+__global__ void ray_initial_kernel(Field F, int64_t nsource, const double* __restrict__ slon,
+                                   const double* __restrict__ slat,
+                                   const double* __restrict__ scos, int32_t nzwn,
+                                   const double* __restrict__ zc, double* __restrict__ rows,
+                                   int32_t* __restrict__ info) {
+  const int64_t n = nsource * nzwn;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t s = i / nzwn;
+    const int iz = (int)(i - s * nzwn);
+    const double lon = slon[s], lat = slat[s];
+    // BS.cal_bs_mercator_point at the source: fmu fmv fmqx fmqy (bs.py:856-883)
+    double fu, fv, fqx, fqy;
+    interp4(F, py_mod_2pi(lon), lat, fu, fv, fqx, fqy);
+    const Merc M = merc_factors(lat, scos[s], 0.0);
+    const double fmu = (fu / M.cp) * M.m;
+    const double fmv = (fv / M.cp) * M.m;
+    const double fmqx = fqx * M.m;
+    const double fmqy = (fqy * M.cp) * M.m;
+    const double k = zc[iz], k2 = zc[nzwn + iz], k3 = zc[2 * nzwn + iz], ps = zc[3 * nzwn + iz];
+    double mr[3] = {kNaN, kNaN, kNaN};
+    if (k != 0.0) {
+      // cal_ky_numpy coefficients, lowest order first (bs.py:1005-1012)
+      const double c[4] = {k3 * ((fmu - ps) - (fmqy / k2)), k2 * fmv + fmqx, k * (fmu - ps), fmv};
+      int deg = 3;
+      while (deg > 0 && fabs(c[deg]) == 0.0) --deg;    // exact-zero reduction
+      if (deg >= 1) {
+        double p[4];
+        for (int q = 0; q <= deg; ++q) p[q] = c[deg - q];   // highest first
+        nproots::cx r[3] = {{kNaN, kNaN}, {kNaN, kNaN}, {kNaN, kNaN}};
+        bool finite = true;
+        for (int q = 0; q <= deg; ++q) finite = finite && isfinite(p[q]);
+        int st = finite ? nproots::np_roots(p, deg, r) : -1;
+        if (st != 0) atomicAdd(info, 1);   // np.linalg.eigvals would raise
+        // real roots (|Im| < delt), compacted in np.roots' order (bs.py:1030-1036)
+        int nreal = 0;
+        for (int q = 0; q < deg; ++q)
+          if (st == 0 && fabs(r[q].im) < 1e-8) mr[nreal++] = r[q].re;
+        order_roots(mr, nreal);
+      }
+    }
+    // outputs: rows[v][slot][s][iz]
+    const int64_t plane = 3 * n;
+    for (int slot = 0; slot < 3; ++slot) {
+      const double m = mr[slot];
+      const int64_t o = (int64_t)slot * n + i;
+      double ug, vg;
+      if (k == 0.0) {
+        ug = 0.0;
+        vg = 0.0;
+      } else {
+        // cal_ugvg_numpy (wn.py:209-259)
+        double nans = ((m * 0.0) * (((fmu * fmqx) * fmqy) * 0.0)) + 1.0;
+        if (isnan(nans)) nans = 0.0;
+        const double a = (k * k) - (m * m);
+        const double b = (2.0 * k) * m;
+        const double cc = (k * k) + (m * m);
+        const double c2 = cc * cc;
+        ug = (fmu + (((a * fmqy) - (b * fmqx)) / c2)) * nans;
+        vg = (fmv + (((a * fmqx) + (b * fmqy)) / c2)) * nans;
+      }
+      rows[0 * plane + o] = lon;
+      rows[1 * plane + o] = lat;
+      rows[2 * plane + o] = k;
+      rows[3 * plane + o] = m;
+      rows[4 * plane + o] = isnan(m) ? kNaN : 1.0;
+      rows[5 * plane + o] = ug;
+      rows[6 * plane + o] = vg;
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Host side of the ABI
 // ---------------------------------------------------------------------------
@@ -1185,6 +1283,24 @@ rwrt_status rwrt_dp54_attempt(const rwrt_grid* g, const double* d_packed, int64_
   hipLaunchKernelGGL(attempt_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, F,
                      n, d_y, d_f, d_h, rtol, atol, d_K, d_ynew, d_err);
   return check_launch("attempt_kernel");
+}
+
+rwrt_status rwrt_ray_initial(const rwrt_grid* g, const double* d_packed, int64_t nsource,
+                             const double* d_src_lon, const double* d_src_lat,
+                             const double* d_src_cos, int32_t nzwn, const double* d_zwn,
+                             double* d_rows, int32_t* d_info, void* stream) {
+  Field F;
+  if (rwrt_status s = make_field(g, d_packed, F)) return s;
+  if (nsource < 0 || nzwn < 0) return fail(RWRT_ERR_ARG, "negative size%s");
+  if (!d_src_lon || !d_src_lat || !d_src_cos || !d_zwn || !d_rows || !d_info)
+    return fail(RWRT_ERR_ARG, "NULL buffer%s");
+  if (hipMemsetAsync(d_info, 0, sizeof(int32_t), (hipStream_t)stream) != hipSuccess)
+    return check_launch("hipMemsetAsync(info)");
+  const int64_t n = nsource * (int64_t)nzwn;
+  if (n == 0) return RWRT_OK;
+  hipLaunchKernelGGL(ray_initial_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream,
+                     F, nsource, d_src_lon, d_src_lat, d_src_cos, nzwn, d_zwn, d_rows, d_info);
+  return check_launch("ray_initial_kernel");
 }
 
 rwrt_status rwrt_rk45_init(const rwrt_grid* g, const double* d_packed, int64_t nray,

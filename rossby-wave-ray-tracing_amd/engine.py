@@ -9,6 +9,7 @@ import numpy as np
 import torch
 
 import _hip as H
+from constants import rearth as R_EARTH
 
 F64 = torch.float64
 
@@ -103,6 +104,59 @@ class RayEngine:
                                            H.dptr(f), H.dptr(h), rtol, atol, H.dptr(K),
                                            H.dptr(yn), H.dptr(err), H.stream()))
         return K, yn, err
+
+    # ------------------------------------------------------- initial rays
+    @staticmethod
+    def zwn_constants(zwn, freq):
+        """``{k, k**2, k**3, freq/k*R}`` per zonal wavenumber, evaluated by NumPy
+        exactly as ``cal_ky_numpy`` does (bs.py:1005-1012): ``[4, nzwn]``."""
+        freq = np.atleast_1d(np.asarray(freq, np.float64))
+        zc = np.zeros((4, len(zwn)))
+        for iz, kz in enumerate(np.asarray(zwn, np.float64)):
+            zc[0, iz] = kz
+            zc[1, iz] = kz ** 2
+            zc[2, iz] = kz ** 3
+            with np.errstate(all="ignore"):
+                zc[3, iz] = (freq / kz * R_EARTH)[0]
+        return zc
+
+    def sources(self, source_lon, source_lat):
+        """Device inputs of rwrt_ray_initial for a source list: lon, lat and the
+        host-libm ``np.cos(lat)`` (``[3, nsource]``)."""
+        slat = np.ascontiguousarray(source_lat, dtype=np.float64)
+        s = np.stack([np.ascontiguousarray(source_lon, dtype=np.float64), slat, np.cos(slat)])
+        return torch.as_tensor(s, dtype=F64).to(self.device)
+
+    def zwn_tensor(self, zwn, freq):
+        return torch.as_tensor(self.zwn_constants(zwn, freq), dtype=F64).to(self.device)
+
+    def initial_rows_dev(self, src, zc, rows=None, info=None):
+        """Launch rwrt_ray_initial on resident inputs (``sources``, ``zwn_tensor``);
+        returns ``(rows[7, 3, nsource, nzwn], info[1])`` without synchronising."""
+        ns, nz = src.shape[1], zc.shape[1]
+        if rows is None:
+            rows = torch.empty((7, 3, ns, nz), dtype=F64, device=self.device)
+        if info is None:
+            info = torch.zeros(1, dtype=torch.int32, device=self.device)
+        H.check(H.load().rwrt_ray_initial(self.grid, H.dptr(self.packed), ns, H.dptr(src[0]),
+                                          H.dptr(src[1]), H.dptr(src[2]), nz, H.dptr(zc),
+                                          H.dptr(rows), H.dptr(info), H.stream()))
+        return rows, info
+
+    def initial_rows(self, source_lon, source_lat, zwn, freq, check=True):
+        """``WR.ray_initial_numpy`` (wr.py:344-395) on the GPU: the device tensor
+        ``rows[7, 3, nsource, nzwn]`` = lon lat k l amp ug vg.  Bit-identical
+        to the host path (np.roots restated in csrc/nproots.h); the source
+        ``cos(lat)`` comes from the host libm, as in the reference.  With
+        ``check`` (default), non-finite dispersion coefficients raise like
+        ``np.linalg.eigvals`` does in the reference."""
+        src = self.sources(source_lon, source_lat)
+        rows, info = self.initial_rows_dev(src, self.zwn_tensor(zwn, freq))
+        if check and int(info.item()) != 0:
+            raise np.linalg.LinAlgError(
+                f"Array must not contain infs or NaNs ({int(info.item())} dispersion "
+                f"polynomials with non-finite coefficients; np.roots raises here too)")
+        return rows
 
     # ------------------------------------------------------------ ray loop
     @staticmethod

@@ -125,9 +125,23 @@ class WR:
                          self.rvg), rows):
             h[0] = r
 
+    def ray_initial_hip(self):
+        """Initial rows on the GPU (``RayEngine.initial_rows``): bit-identical to
+        ``ray_initial_numpy`` -- np.roots' companion-matrix eigenvalues restated
+        operation for operation on the device (csrc/nproots.h)."""
+        rows = self.bs.engine().initial_rows(self.source_lon, self.source_lat, self.zwn,
+                                             self.freq).cpu().numpy()
+        for h, r in zip((self.rlon, self.rlat, self.rzwn, self.rmwn, self.ramp, self.rug,
+                         self.rvg), rows):
+            h[0] = r
+
     def ray_initial(self, mode="numpy", root_method="numpy"):
-        """The vectorised initialiser of the reference's RK45 path (mode 'numpy')."""
-        self.ray_initial_numpy(root_method=root_method)
+        """Initial rays (wr.py:417-421): ``mode='numpy'`` is the reference's
+        vectorised host initialiser, ``mode='hip'`` the same on the GPU."""
+        if mode == "hip":
+            self.ray_initial_hip()
+        else:
+            self.ray_initial_numpy(root_method=root_method)
 
     # ---------------------------------------------------------- ray loop
     def core_ray_run_hip_rk45(self, group=None):
@@ -209,7 +223,7 @@ class WR:
         key = mode + "_rk45" if inte_method == "rk45" else mode
         if key not in SUPPORTED:
             self.core_ray_run(key)     # raises before any work
-        self.ray_initial(mode="numpy", root_method=root_method)
+        self.ray_initial(mode=mode, root_method=root_method)   # wr.py:900 (mode 'hip': GPU)
         if debug and debug_file is not None:
             try:
                 self.load_init_from_precal_nc(debug_file)

@@ -136,6 +136,57 @@ def test_initial_step(kind):
     assert live.sum() == int(st["summary"][0])
 
 
+# ------------------------------------------------------------ initial rays
+def same_bits(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    return a.shape == b.shape and np.array_equal(a, b, equal_nan=True)
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_initial_rows_gpu_bitwise_c2(kind):
+    """rwrt_ray_initial (Mercator point, np.roots restated, change_roots_order,
+    t = 0 group velocity) == the reference's row 0 of C2, bit for bit."""
+    from wr import WR
+    g = golden(f"init_C2_{kind}.npz")
+    cfg = S.config("C2")
+    w = WR(cfg.nzwn, cfg.nsource, 7200.0, 7200.0, cfg.freq, nx=144, ny=73)
+    w.set_source_matrix(cfg.SW_lon, cfg.SW_lat, cfg.dlon, cfg.dlat, cfg.nnx, cfg.nny)
+    rows = engine(kind).initial_rows(w.source_lon, w.source_lat, cfg.zwn, cfg.freq)
+    assert same_bits(rows.cpu().numpy(), g["rows"])
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_initial_rows_gpu_bitwise_c3_golden(kind):
+    """The reference's C3 roots subsample (stationary and 10-day waves): m, amp,
+    ug, vg bit-identical -- including the ORDER of the three roots."""
+    g = golden("roots_C3.npz")
+    cfg = S.config("C3")
+    for tag in ("stat", "p10"):
+        src = g[f"{tag}_{kind}_src"]
+        rows = engine(kind).initial_rows(src[0], src[1], cfg.zwn, float(g[f"{tag}_{kind}_freq"]))
+        got = rows.cpu().numpy()[[3, 4, 5, 6]]
+        assert same_bits(got, g[f"{tag}_{kind}_rows"]), tag
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_initial_rows_gpu_equals_host_full_c3(kind):
+    """All 2.40 M C3 slots (5 periods): GPU rows == host rows (the host path is
+    bit-exact with the reference, tests/test_host_prep.py)."""
+    from wr import initial_rows
+    cfg = S.config("C3")
+    bs = bs_of(kind)
+    ix, iy = np.meshgrid(np.arange(cfg.nnx), np.arange(cfg.nny))
+    lon = ((cfg.SW_lon % 360.0 + ix.ravel() * cfg.dlon) % 360.0) * (np.pi / 180.0)
+    lat = (cfg.SW_lat + iy.ravel() * cfg.dlat) * (np.pi / 180.0)
+    for P in S.C3_PERIODS_DAYS:
+        f = S.c3_freq(P)
+        with np.errstate(all="ignore"):
+            host = np.array(initial_rows(bs, lon, lat, cfg.zwn, f))
+        dev = engine(kind).initial_rows(lon, lat, cfg.zwn, f).cpu().numpy()
+        bad = ~((dev == host) | (np.isnan(dev) & np.isnan(host)))
+        assert not bad.any(), (P, int(bad.sum()))
+
+
 # ------------------------------------------------------------------- T2 / T3
 def run_c2(kind, nt, chunk=None, order=None):
     from engine import t_eval_of
