@@ -123,6 +123,11 @@ def main():
                     help="rows of the short leading launches that measure per-ray cost (comma list)")
     ap.add_argument("--init", default="gpu", choices=["gpu", "host"],
                     help="initial rows: GPU kernel inside each step (default) or host rows resident")
+    ap.add_argument("--config", default="C3", choices=["C3", "C5"],
+                    help="C3 (BASELINE configs[2], the metric's workload) or C5 (configs[4]: "
+                         "0.25-degree time-varying background, ~3.9 M ray slots)")
+    ap.add_argument("--fields", default="fp64", choices=["fp64", "fp32"],
+                    help="C5: storage of the background levels (arithmetic is fp64 either way)")
     ap.add_argument("--lib", default=None, help="alternative librwrt build (A/B timing)")
     ap.add_argument("--traffic", default=None,
                     help="traffic.json from tools/pmc_traffic.py (default: newest profiles/*/traffic.json "
@@ -143,6 +148,8 @@ def main():
         dist.init_process_group("nccl")
     dev = torch.device("cuda", local if world > 1 else 0)
 
+    if args.config == "C5":
+        return main_c5(args, dist, rank, world, dev)
     from engine import RayEngine
     bs, bg = make_bs("zonal")
     periods = S.C3_PERIODS_DAYS[: args.periods]
@@ -274,6 +281,117 @@ def main():
                                "alive_mismatch": int(np.sum(np.isnan(g[:, 0]) != np.isnan(c[:, 0])))})
             result["max_dpos_vs_cpu_rad"] = parity
         print(json.dumps(result))
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def main_c5(args, dist, rank, world, dev):
+    """BASELINE configs[4] on one GPU per rank: a 0.25-degree time-varying
+    background (one level every 6 h, built on the device by rwrt_bs_ready,
+    fp64 or fp32 storage) and 1-degree global seeds x k = 1..10 x periods
+    {stationary, 10 d} (3.87 M ray slots), 90 days at 2 h.  One step = GPU
+    initial rows + the time-varying ray loop; levels and sources are resident
+    in HBM before the timed region.  Rays shard like C3 (weak scaling)."""
+    from engine import RayEngine
+    from levels import Levels
+    res, dt_bg = 0.25, 6 * 3600.0
+    nt = int(round(args.days * 12)) + 1
+    nlev = int(np.ceil((nt - 1) * 7200.0 / dt_bg)) + 1
+    b0 = S.background_level(0, res=res)
+    t_build = time.perf_counter()
+    lv = Levels(b0["lat"], b0["lon"], nlev, t0=0.0, dt=dt_bg, fp32=(args.fields == "fp32"), device=dev)
+    for j in range(nlev):
+        bj = b0 if j == 0 else S.background_level(j, res=res)
+        lv.set_level(j, bj["u"], bj["v"])
+    torch.cuda.synchronize()
+    t_build = time.perf_counter() - t_build
+    eng = RayEngine.from_levels(lv)
+    cfg = S.config("C5")
+    deg2rad = np.pi / 180.0
+    ix, iy = np.meshgrid(np.arange(cfg.nnx), np.arange(cfg.nny))
+    lon_off = rank * 1.0 / max(world, 1)
+    lon = (((cfg.SW_lon + lon_off) % 360.0 + ix.ravel() * cfg.dlon) % 360.0) * deg2rad
+    lat = (cfg.SW_lat + iy.ravel() * cfg.dlat) * deg2rad
+    src = eng.sources(lon, lat)
+    zcs = [eng.zwn_tensor(cfg.zwn, S.c3_freq(P)) for P in S.C5_PERIODS_DAYS]
+    rows = [None] * len(zcs)
+
+    def make_y0():
+        ys = []
+        for j, zc in enumerate(zcs):
+            rows[j], _ = eng.initial_rows_dev(src, zc, rows[j])
+            ys.append(rows[j][:5].reshape(5, -1))
+        return torch.cat(ys, dim=1)
+
+    y0 = make_y0()
+    nslot = y0.shape[1]
+    n_live = int((~torch.isnan(y0.sum(0))).sum().item())
+    chunk = args.chunk or 12          # one day per launch: <= 5 levels in flight (L2/MALL window)
+    out = torch.empty((nslot, min(chunk, nt - 1), 8), dtype=torch.float64, device=dev)
+
+    def one_step(events=None):
+        return eng.integrate(make_y0(), nt, 7200.0, ttotal=(nt - 1) * 7200.0, chunk=chunk, out=out,
+                             events=events, order_policy=args.order,
+                             first_chunk=[int(x) for x in str(args.first_chunk).split(",") if x])
+
+    for _ in range(args.warmup):
+        one_step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    events, steps_done = [], 0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        r = one_step(events)
+        steps_done += r.ray_steps
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_s = sum(a.elapsed_time(b) for a, b in events) / 1e3
+    tot_steps, max_el = steps_done, elapsed
+    if dist:
+        t = torch.tensor([float(steps_done), elapsed], dtype=torch.float64, device=dev)
+        s, m = t.clone(), t.clone()
+        dist.all_reduce(s, op=dist.ReduceOp.SUM)
+        dist.all_reduce(m, op=dist.ReduceOp.MAX)
+        tot_steps, max_el = s[0].item(), m[1].item()
+    if rank == 0:
+        fbytes = 4 if lv.fp32 else 8
+        bps = 6 * 4 * 11 * fbytes * 2          # 6 RHS x 4 corners x 11 fields x 2 levels
+        per_launch_steps = steps_done / max(len(events), 1)
+        avg_launch_s = kern_s / max(len(events), 1)
+        achieved = per_launch_steps * bps / avg_launch_s
+        workload = (f"C5: 1deg global seeds x k=1..10 x 2 periods, {args.days:g} d at 2 h, 0.25deg "
+                    f"time-varying background ({nlev} levels every 6 h, {args.fields} storage; "
+                    f"BASELINE configs[4])")
+        schedule = [b - a for a, b in r.bounds]
+        traffic, tsrc = find_traffic(args.traffic, workload, schedule)
+        print(json.dumps({
+            "metric": METRIC, "value": tot_steps / max_el, "unit": "ray-steps/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * max_el / args.steps,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic",
+            "config": {"workload": workload, "ray_slots_per_gpu": nslot, "live_rays_per_gpu": n_live,
+                       "rows": nt, "levels": nlev, "field_storage": args.fields,
+                       "level_bytes": int(lv.packed[0].numel() * lv.packed.element_size()),
+                       "rows_per_launch": chunk, "launch_rows": schedule,
+                       "parallelism": f"rays sharded, {world} rank(s), 1 GPU each"},
+            "ray_steps_per_step": steps_done / args.steps,
+            "rejected_per_accepted": int(r.nrej.sum().item()) / max(r.ray_steps, 1),
+            "levels_build_s": t_build,
+            "init": "GPU rwrt_ray_initial inside every timed step",
+            "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK,
+                         "traffic": traffic["traffic_bytes_per_launch"] if traffic else None,
+                         "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
+                         "traffic_source": tsrc,
+                         "algorithmic_bytes_per_launch": per_launch_steps * bps,
+                         "kernel": "rk45_run_kernel", "avg_launch_ms": 1e3 * avg_launch_s,
+                         "launches": len(events), "bytes_per_ray_step": bps}}))
     if dist:
         dist.barrier()
         dist.destroy_process_group()

@@ -62,6 +62,20 @@ typedef struct {
   double tstep;     /* output interval = RK4 step  wr.py:147       */
 } rwrt_params;
 
+/* A time-varying basic state (this framework's extension for BASELINE
+ * configs[4]; the reference's fun ignores t, wr.py:784-789): nlev packed
+ * levels [nlev][ncol][nrow][12] (fp64, or fp32 when fp32 != 0) valid at
+ * t0 + j*dt seconds of ray time.  The RHS interpolates each level bilinearly
+ * exactly like the static state and then linearly in time:
+ * s = (t - t0)/dt, j = clip(floor(s), 0, nlev-2), w = clip(s - j, 0, 1),
+ * field = f_j (1 - w) + f_{j+1} w. */
+typedef struct {
+  const void* d_levels;
+  int32_t nlev;
+  int32_t fp32;
+  double t0;
+  double dt;
+} rwrt_background;
 const char* rwrt_version(void);
 /* Last error message of the calling thread ("" if none). */
 const char* rwrt_last_error(void);
@@ -165,6 +179,39 @@ rwrt_status rwrt_rk4_run(const rwrt_grid* g, const double* d_packed,
                          double* d_state, int64_t* d_count, int32_t* d_nanrow,
                          double* d_out, int32_t* d_work, void* stream);
 
+/* BS.ready on the device (bs.py:264-279 vorticity, bs.py:121-200 finite
+ * differences, bs.py:291-305 smth9, bs.py:318-372 the stack): writes the
+ * packed record [nlon+1][nlat][12] of one basic state (fp64, or fp32 when
+ * fp32 != 0) -- the 11 hot fields bit-identical to BS.fields.
+ *  d_u, d_v [nlat][nlon] float32 as read from the file (ascending latitude;
+ *    the host flips a descending file like bs.py:251-256).
+ *  d_trig[3][nlat]: np.cos(lat) (for u cos(lat)), then np.cos and np.sin of
+ *    lat[1:-1] at indices 1..nlat-2 (host libm, the reference's values).
+ *  dx, dy: BS.dx, BS.dy (bs.py:77-78).  d_scratch: 4*nlon*nlat doubles. */
+rwrt_status rwrt_bs_ready(int32_t nlon, int32_t nlat, const float* d_u,
+                          const float* d_v, const double* d_trig, double dx,
+                          double dy, double* d_scratch, void* d_packed,
+                          int32_t fp32, void* stream);
+/* rwrt_rk45_init / rwrt_rk45_run on a time-varying background (same state,
+ * queue and output conventions).  Steps reuse K6 = fun(t + h, y_new) as the
+ * next f (FSAL, scipy's RK45 convention); the per-row group velocity is
+ * evaluated at the row time t_bound. */
+rwrt_status rwrt_rk45_init_tv(const rwrt_grid* g, const rwrt_background* b,
+                              int64_t nray, const double* d_y0,
+                              const rwrt_params* p, double* d_state,
+                              int64_t* d_count, int32_t* d_nanrow,
+                              int32_t* d_live, int64_t* d_summary, void* stream);
+rwrt_status rwrt_rk45_run_tv(const rwrt_grid* g, const rwrt_background* b,
+                             int64_t nray, const rwrt_params* p,
+                             const double* d_tbound, int32_t it_begin,
+                             int32_t it_end, const int64_t* d_order,
+                             int64_t n_heavy, double* d_state, int64_t* d_count,
+                             int32_t* d_nanrow, double* d_out, int32_t* d_work,
+                             void* stream);
+/* The time-varying RHS at per-point times: d_t[n], d_y[5][n] -> d_dydt[5][n]. */
+rwrt_status rwrt_rhs_tv(const rwrt_grid* g, const rwrt_background* b, int64_t n,
+                        const double* d_t, const double* d_y, double* d_dydt,
+                        void* stream);
 /* Stepper known-answer tests: the same device stepper on the analytic ODEs of
  * the rkf45.py demos (rkf45.py:839-882), driven like rk45_simple_current
  * (rkf45.py:672-724).  kind: 0 dx/dt = 2t, 1 dx/dt = e^(0.1 t), 2 Lorenz

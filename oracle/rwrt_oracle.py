@@ -150,19 +150,60 @@ class Background:
         return f
 
 
+class TimeVaryingBackground:
+    """Time-varying basic state -- THIS FRAMEWORK'S EXTENSION, not in the reference
+    (its ``fun`` ignores ``t``, wr.py:784-789).  Parity of
+    the extension is against this restatement; its building blocks are the
+    reference's (``Background`` per level, bilinear ``_cell``), and at a level
+    time ``t0 + j*dt`` it returns level ``j``'s values bit for bit.
+
+    Per point: ``s = (t - t0)/dt``, ``j = clip(floor(s), 0, nlev-2)``,
+    ``w = clip(s - j, 0, 1)``, ``g = g_j (1 - w) + g_{j+1} w`` after the bilinear
+    lookup of each level (include/rwrt.h ``rwrt_background``).  ``fp32``: the
+    levels are stored in float32 (rounded once), arithmetic stays float64.
+    Only the 11 fields the ray path reads are carried (the others are NaN).
+    """
+    HOT = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 11]
+
+    def __init__(self, levels, t0=0.0, dt=6 * HOUR, fp32=False):
+        self.lat, self.lon = levels[0].lat, levels[0].lon
+        F = np.stack([b.fields for b in levels])                    # (nlev, W, H, 18)
+        if fp32:
+            F = F.astype(np.float32).astype(np.float64)
+        mask = np.zeros(F.shape[-1], bool)
+        mask[self.HOT] = True
+        F[..., ~mask] = np.nan
+        self.F = F
+        self.fields = F[0]
+        self.nlev, self.t0, self.dt = len(levels), float(t0), float(dt)
+
+    def interp_time(self, c, t):
+        s = (t - self.t0) / self.dt
+        j = np.floor(s).astype("int32")
+        j = np.clip(j, 0, self.nlev - 2) if self.nlev > 1 else np.zeros_like(j)
+        w = np.clip(s - j, 0.0, 1.0)
+        jb = j + 1 if self.nlev > 1 else j
+        ok, x0, x1, y0, y1, wa, wb, wc, wd = c
+        F = self.F
+        ga = (F[j, x0, y1] * wa[:, None] + F[j, x1, y1] * wb[:, None]
+              + F[j, x0, y0] * wc[:, None] + F[j, x1, y0] * wd[:, None])
+        gb = (F[jb, x0, y1] * wa[:, None] + F[jb, x1, y1] * wb[:, None]
+              + F[jb, x0, y0] * wc[:, None] + F[jb, x1, y0] * wd[:, None])
+        return ga * (1.0 - w)[:, None] + gb * w[:, None]
+
+
 # ----------------------------------------------------------------------------
 # interpolation + Mercator conversion
 # ----------------------------------------------------------------------------
-def mercator_point(bg, lon, lat):
-    """``BS.cal_bs_mercator_point(lon, lat, mode='numpy')``: returns ``(18, N)``."""
-    F = bg.fields
+def _cell(bg, lon, lat):
+    """Bilinear cell of ``batch_linint2_metpy`` (interpolation.py:77-135) for the
+    in-range points: ``(ok, x0, x1, y0, y1, wa, wb, wc, wd)``."""
     lon = lon % (2 * PI)                                  # bs.py:519
     ok = np.where(np.abs(lat) <= 0.5 * PI)[0]             # bs.py:787
-    vals = np.full((F.shape[-1], len(lat)), np.nan)
     xs = lon[ok] % (2 * np.pi)                            # interpolation.py:80
     fx = (xs - bg.lon[0]) / (bg.lon[1] - bg.lon[0])
     fy = (lat[ok] - bg.lat[0]) / (bg.lat[1] - bg.lat[0])
-    W, H = F.shape[0], F.shape[1]
+    W, H = bg.fields.shape[-3], bg.fields.shape[-2]
     ix = np.floor(fx).astype("int32")
     iy = np.floor(fy).astype("int32")
     x0, x1 = np.clip(ix, 0, W - 1), np.clip(ix + 1, 0, W - 1)
@@ -170,9 +211,26 @@ def mercator_point(bg, lon, lat):
     sx, sy = fx - x0, fy - y0
     wa, wb = (1 - sx) * sy, sx * sy
     wc, wd = (1 - sx) * (1 - sy), sx * (1 - sy)
-    g = (F[x0, y1] * wa[:, None] + F[x1, y1] * wb[:, None]
-         + F[x0, y0] * wc[:, None] + F[x1, y0] * wd[:, None])
-    vals[:, ok] = g.T
+    return ok, x0, x1, y0, y1, wa, wb, wc, wd
+
+
+def _bilinear(F, c):
+    ok, x0, x1, y0, y1, wa, wb, wc, wd = c
+    return (F[x0, y1] * wa[:, None] + F[x1, y1] * wb[:, None]
+            + F[x0, y0] * wc[:, None] + F[x1, y0] * wd[:, None])
+
+
+def mercator_point(bg, lon, lat, t=None):
+    """``BS.cal_bs_mercator_point(lon, lat, mode='numpy')``: returns ``(18, N)``.
+
+    ``t`` (per point) is read only by a ``TimeVaryingBackground``."""
+    c = _cell(bg, lon, lat)
+    ok = c[0]
+    vals = np.full((bg.fields.shape[-1], len(lat)), np.nan)
+    if isinstance(bg, TimeVaryingBackground):
+        vals[:, ok] = bg.interp_time(c, np.broadcast_to(t, lat.shape)[ok]).T
+    else:
+        vals[:, ok] = _bilinear(bg.fields, c).T
     (fu, fv, fux, fuy, fvx, fvy, fqx, fqy, fqxx, fqxy, fqyx, fqyy,
      fqxxx, fqxxy, fqxyy, fqyyy, fqyxx, fqyyx) = vals
     c, s, t = np.cos(lat), np.sin(lat), np.tan(lat)
@@ -199,13 +257,14 @@ def ugvg_extent(fu, fv, fqx, fqy, k, l):
     return ug, vg
 
 
-def rhs(bg, y):
-    """``WR.diffun_numpy`` on ``y[5, N]`` -> ``(dydt[5, N], bad[N])``."""
+def rhs(bg, y, t=None):
+    """``WR.diffun_numpy`` on ``y[5, N]`` -> ``(dydt[5, N], bad[N])`` (``t``: time
+    of each column, read only by a ``TimeVaryingBackground``)."""
     lon, lat, kx, ky, amp = y[0], y[1], y[2], y[3], y[4]
     bad = (np.abs(lat) >= 0.5 * PI) | (np.abs(ky) >= 100.0)          # wr.py:508-510
     ky = ky.copy()
     ky[bad] = np.nan
-    M = mercator_point(bg, lon.reshape(-1), lat.reshape(-1))
+    M = mercator_point(bg, lon.reshape(-1), lat.reshape(-1), t)
     fmu, fmv, fmux, fmuy, fmvx, fmvy, fmqx, fmqy, fmqxx, fmqxy, fmqyx, fmqyy = M[:12]
     ug, vg = ugvg_extent(fmu, fmv, fmqx, fmqy, kx, ky)
     # wr.py:44-82 core_diffun
@@ -390,7 +449,7 @@ def ray_run(bg, y0, nt, tstep, rtol=1e-6, atol=1e-6, msf=1e-3, cut_off=0.1,
     ``status`` is 0, or -1 when the solver failed (remaining rows NaN,
     wr.py:886-887).
     """
-    fun = lambda t, y: rhs(bg, y)[0]
+    fun = lambda t, y: rhs(bg, y, t)[0]   # FSAL (DP54 autonomous=True) for both backgrounds
     nray = y0.shape[1]
     hist = np.full((7, nt, nray), np.nan)
     if row0 is not None:
@@ -415,7 +474,7 @@ def ray_run(bg, y0, nt, tstep, rtol=1e-6, atol=1e-6, msf=1e-3, cut_off=0.1,
         y[:, np.abs(cal_dis(y[0], y[1], hist[0, i - 1], hist[1, i - 1])) >= cut] = np.nan
         if np.isnan(y[0]).all() or (np.abs(y[1]) > 0.5 * PI).all():     # wr.py:853-855
             break
-        M = mercator_point(bg, y[0], y[1])
+        M = mercator_point(bg, y[0], y[1], np.full(nray, t_eval[i]))   # at the row time
         ug, vg = ugvg_extent(M[0], M[1], M[6], M[7], y[2], y[3])
         hist[:5, i] = y
         hist[5, i], hist[6, i] = ug, vg

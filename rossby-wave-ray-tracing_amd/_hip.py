@@ -16,6 +16,7 @@ NFIELD_REF, NFIELD_PACK, NVAR, NMERC, NOUT, NSTATE = 18, 12, 5, 12, 8, 12
 ABI_SYMBOLS = ("rwrt_version", "rwrt_last_error", "rwrt_pack_fields",
                "rwrt_mercator_point", "rwrt_rhs", "rwrt_dp54_attempt",
                "rwrt_ray_initial", "rwrt_rk45_init", "rwrt_rk45_run", "rwrt_rk4_run",
+               "rwrt_bs_ready", "rwrt_rk45_init_tv", "rwrt_rk45_run_tv", "rwrt_rhs_tv",
                "rwrt_kat_rk45", "rwrt_selftest_math")
 
 RWRT_OK, RWRT_ERR_ARG, RWRT_ERR_HIP, RWRT_SOLVER_FAILED = 0, 1, 2, 3
@@ -42,6 +43,11 @@ class Params(ctypes.Structure):
                 ("tstep", ctypes.c_double)]
 
 
+class Background(ctypes.Structure):
+    _fields_ = [("d_levels", ctypes.c_void_p), ("nlev", ctypes.c_int32), ("fp32", ctypes.c_int32),
+                ("t0", ctypes.c_double), ("dt", ctypes.c_double)]
+
+
 _lib = None
 _P = ctypes.c_void_p
 _I64 = ctypes.c_int64
@@ -60,7 +66,7 @@ def load():
     lib = ctypes.CDLL(LIB_PATH)
     lib.rwrt_version.restype = ctypes.c_char_p
     lib.rwrt_last_error.restype = ctypes.c_char_p
-    G, Pr = ctypes.POINTER(Grid), ctypes.POINTER(Params)
+    G, Pr, B = ctypes.POINTER(Grid), ctypes.POINTER(Params), ctypes.POINTER(Background)
     sig = {
         "rwrt_pack_fields": [G, _P, _P, _P],
         "rwrt_mercator_point": [G, _P, _I64, _P, _P, _P, _P],
@@ -70,6 +76,10 @@ def load():
         "rwrt_rk45_init": [G, _P, _I64, _P, Pr, _P, _P, _P, _P, _P, _P],
         "rwrt_rk45_run": [G, _P, _I64, Pr, _P, _I32, _I32, _P, _I64, _P, _P, _P, _P, _P, _P],
         "rwrt_rk4_run": [G, _P, _I64, Pr, _I32, _I32, _P, _P, _P, _P, _P, _P, _P],
+        "rwrt_bs_ready": [_I32, _I32, _P, _P, _P, _D, _D, _P, _P, _I32, _P],
+        "rwrt_rk45_init_tv": [G, B, _I64, _P, Pr, _P, _P, _P, _P, _P, _P],
+        "rwrt_rk45_run_tv": [G, B, _I64, Pr, _P, _I32, _I32, _P, _I64, _P, _P, _P, _P, _P, _P],
+        "rwrt_rhs_tv": [G, B, _I64, _P, _P, _P, _P],
         "rwrt_kat_rk45": [_I32, _I64, _P, _I32, _P, _D, _D, _D, _P, _P],
         "rwrt_selftest_math": [_I32, _I64, _P, _P, _P, _P],
     }

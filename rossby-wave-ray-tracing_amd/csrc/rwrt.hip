@@ -30,6 +30,7 @@ constexpr double kPi = 3.14159265358979323846;
 constexpr double kHalfPi = 0.5 * kPi;  // "0.5 * pi"  wr.py:508, bs.py:787
 constexpr double kTwoPi = 2.0 * kPi;   // "2 * pi"    bs.py:519, interpolation.py:80
 constexpr double kREarth = 6.3712e6;
+constexpr double kOmega = 7.2921e-5;   // constants.py omega
 constexpr double kRInv = 1.0 / 6.3712e6;   // RN(1 / R)
 
 // x / R correctly rounded without the division sequence (Markstein): q0 is
@@ -238,6 +239,115 @@ __device__ __forceinline__ void interp4(const Field& F, double lon, double lat,
   fqy = blend(k, a1.y, b1.y, c1.y, d1.y);
 }
 
+// ---------------------------------------------------------------------------
+// Backgrounds the RHS reads.  StaticBG is the reference's (one basic state,
+// fun ignores t: wr.py:784-789).  VaryingBG<T> is this framework's extension
+// for time-varying flows (BASELINE configs[4]): nlev
+// packed levels at t0 + j*dt, each interpolated bilinearly in space exactly
+// like the static state, then linearly in time,
+//   s = (t - t0)/dt, j = clip(floor(s), 0, nlev-2), w = clip(s - j, 0, 1),
+//   g = g_j (1 - w) + g_{j+1} w                       (per hot field).
+// T = float stores the levels in fp32 (half the gather bytes; arithmetic
+// stays fp64).  A one-level background never takes this path.
+// ---------------------------------------------------------------------------
+struct StaticBG {
+  static constexpr bool kTimeVarying = false;
+  Field F;
+  __device__ __forceinline__ void interp11(double lon, double lat, double, double g[11]) const {
+    rwrt::interp11(F, py_mod_2pi(lon), lat, g);
+  }
+  __device__ __forceinline__ void interp4(double lon, double lat, double, double& fu, double& fv,
+                                          double& fqx, double& fqy) const {
+    rwrt::interp4(F, py_mod_2pi(lon), lat, fu, fv, fqx, fqy);
+  }
+};
+
+template <class T>
+struct VaryingBG {
+  static constexpr bool kTimeVarying = true;
+  const T* __restrict__ P;   // [nlev][W][H][12]
+  int W, H, nlev;
+  int64_t lev_stride;        // W * H * 12
+  double lon0, dlon, lat0, dlat, t0, dt;
+
+  // cell corners and weights: the arithmetic of corners() (interpolation.py:77-135)
+  __device__ __forceinline__ void cell(double lon, double lat, size_t o[4], double w[4]) const {
+    const double lons = py_mod_2pi_again(py_mod_2pi(lon));
+    const double x = (lons - lon0) / dlon;
+    const double y = (lat - lat0) / dlat;
+    const int64_t ix = floor_i32(x), iy = floor_i32(y);
+    const int x0 = clip(ix, W - 1), x1 = clip(ix + 1, W - 1);
+    const int y0 = clip(iy, H - 1), y1 = clip(iy + 1, H - 1);
+    const double sx = x - (double)x0, sy = y - (double)y0;
+    o[0] = ((size_t)x0 * H + y1) * kNF;   // a = F[x0, y1]
+    o[1] = ((size_t)x1 * H + y1) * kNF;   // b = F[x1, y1]
+    o[2] = ((size_t)x0 * H + y0) * kNF;   // c = F[x0, y0]
+    o[3] = ((size_t)x1 * H + y0) * kNF;   // d = F[x1, y0]
+    w[0] = (1.0 - sx) * sy;
+    w[1] = sx * sy;
+    w[2] = (1.0 - sx) * (1.0 - sy);
+    w[3] = sx * (1.0 - sy);
+  }
+  // level index and weight of time t
+  __device__ __forceinline__ const T* level(double t, double& wt) const {
+    const double s = (t - t0) / dt;
+    const int64_t j = (nlev > 1) ? (int64_t)clip(floor_i32(s), nlev - 2) : 0;
+    wt = np_min(np_max(s - (double)j, 0.0), 1.0);
+    return P + j * lev_stride;
+  }
+  __device__ __forceinline__ static double bl(const double w[4], double a, double b, double c,
+                                              double d) {
+    return ((a * w[0] + b * w[1]) + c * w[2]) + d * w[3];
+  }
+  // fields [f0, f0 + n) of one level at the corners
+  template <int N>
+  __device__ __forceinline__ void blend_level(const T* L, const size_t o[4], const double w[4],
+                                              int f0, double* g) const {
+#pragma unroll
+    for (int q = 0; q < N; ++q)
+      g[q] = bl(w, (double)L[o[0] + f0 + q], (double)L[o[1] + f0 + q], (double)L[o[2] + f0 + q],
+                (double)L[o[3] + f0 + q]);
+  }
+  __device__ __forceinline__ void interp11(double lon, double lat, double t, double g[11]) const {
+    if (!(fabs(lat) <= kHalfPi)) {
+#pragma unroll
+      for (int i = 0; i < 11; ++i) g[i] = kNaN;
+      return;
+    }
+    size_t o[4];
+    double w[4], wt;
+    cell(lon, lat, o, w);
+    const T* A = level(t, wt);
+    const T* B = A + (nlev > 1 ? lev_stride : 0);
+    double ga[11], gb[11];
+    blend_level<11>(A, o, w, 0, ga);
+    blend_level<11>(B, o, w, 0, gb);
+#pragma unroll
+    for (int i = 0; i < 11; ++i) g[i] = ga[i] * (1.0 - wt) + gb[i] * wt;
+  }
+  __device__ __forceinline__ void interp4(double lon, double lat, double t, double& fu, double& fv,
+                                          double& fqx, double& fqy) const {
+    if (!(fabs(lat) <= kHalfPi)) {
+      fu = fv = fqx = fqy = kNaN;
+      return;
+    }
+    size_t o[4];
+    double w[4], wt;
+    cell(lon, lat, o, w);
+    const T* A = level(t, wt);
+    const T* B = A + (nlev > 1 ? lev_stride : 0);
+    double a[2], b[2], c[2], d[2];
+    blend_level<2>(A, o, w, F_U, a);
+    blend_level<2>(B, o, w, F_U, b);
+    blend_level<2>(A, o, w, F_QX, c);
+    blend_level<2>(B, o, w, F_QX, d);
+    fu = a[0] * (1.0 - wt) + b[0] * wt;
+    fv = a[1] * (1.0 - wt) + b[1] * wt;
+    fqx = c[0] * (1.0 - wt) + d[0] * wt;
+    fqy = c[1] * (1.0 - wt) + d[1] * wt;
+  }
+};
+
 // Mercator factors of cal_bs_mercator_point (bs.py:856-860).
 struct Merc {
   double c, s, m, cp;
@@ -289,7 +399,8 @@ __device__ __forceinline__ void ugvg(double fu, double fv, double fqx, double fq
 // aux (optional) receives {ug, vg, cos(lat)} of this evaluation -- exactly what
 // the per-interval post-processing recomputes at the same position
 // (wr.py:844, 856-865) -- or NaN for a masked ray (no values computed).
-__device__ __forceinline__ void ray_rhs(const Field& F, const double* y, double* dy,
+template <class BG>
+__device__ __forceinline__ void ray_rhs(const BG& B, double t, const double* y, double* dy,
                                         double* aux = nullptr) {
   const double lon = y[0], lat = y[1], kx = y[2], ky = y[3], amp = y[4];
   // wr.py:508-514 -- a masked ray returns NaN for every derivative (wr.py:552-553)
@@ -300,7 +411,7 @@ __device__ __forceinline__ void ray_rhs(const Field& F, const double* y, double*
     return;
   }
   double g[11];
-  interp11(F, py_mod_2pi(lon), lat, g);
+  B.interp11(lon, lat, t, g);
   double s, c;
   sincos(lat, &s, &c);              // one argument reduction for both (== sin(), cos())
   const double tn = tan(lat);
@@ -335,10 +446,11 @@ __device__ __forceinline__ void ray_rhs(const Field& F, const double* y, double*
 }
 
 // group velocity at a stored position (wr.py:856-865): no |l| mask here
-__device__ __forceinline__ void ugvg_at(const Field& F, double lon, double lat, double k,
+template <class BG>
+__device__ __forceinline__ void ugvg_at(const BG& B, double t, double lon, double lat, double k,
                                         double l, double& ug, double& vg) {
   double fu, fv, fqx, fqy;
-  interp4(F, py_mod_2pi(lon), lat, fu, fv, fqx, fqy);
+  B.interp4(lon, lat, t, fu, fv, fqx, fqy);
   const double c = cos(lat);
   const double m = (fabs(c) <= 0.0175) ? 0.0 : 1.0;
   const double cp = c * m + (1.0 - m) * 1e-6;
@@ -364,16 +476,22 @@ __device__ __forceinline__ double cal_dis_c(double lon_c, double lat_c, double l
 // ---------------------------------------------------------------------------
 // Problems the stepper integrates
 // ---------------------------------------------------------------------------
-struct RayProblem {
+// The step control reuses K6 as the next step's f (FSAL) for both
+// backgrounds: the reference recomputes f = fun(t, y) (rkf45.py:378), which is
+// K6 bit for bit when fun ignores t; for a time-varying flow K6 = fun(t + h,
+// y_new) is scipy's RK45 convention (the reference has no time-varying mode).
+template <class BG>
+struct RayProblemT {
   static constexpr int NV = 5;
   static constexpr int NAUX = 3;             // ug, vg, cos(lat) of the evaluation
-  static constexpr bool kAutonomous = true;  // fun ignores t (wr.py:784-789)
-  Field F;
-  __device__ __forceinline__ void operator()(double, const double* y, double* dy,
+  static constexpr bool kAutonomous = true;  // FSAL (see above)
+  BG B;
+  __device__ __forceinline__ void operator()(double t, const double* y, double* dy,
                                              double* aux = nullptr) const {
-    ray_rhs(F, y, dy, aux);
+    ray_rhs(B, t, y, dy, aux);
   }
 };
+using RayProblem = RayProblemT<StaticBG>;
 
 // rkf45.py demo ODEs (rkf45.py:775-782, 839-841, 861-863)
 struct KatLinear {
@@ -694,7 +812,7 @@ __global__ void rhs_kernel(Field F, int64_t n, const double* __restrict__ y,
     double yy[5], d[5];
 #pragma unroll
     for (int v = 0; v < 5; ++v) yy[v] = y[v * n + i];
-    ray_rhs(F, yy, d);
+    ray_rhs(StaticBG{F}, 0.0, yy, d);
 #pragma unroll
     for (int v = 0; v < 5; ++v) dydt[v * n + i] = d[v];
   }
@@ -704,7 +822,7 @@ __global__ void attempt_kernel(Field F, int64_t n, const double* __restrict__ y,
                                const double* __restrict__ f, const double* __restrict__ h,
                                double rtol, double atol, double* __restrict__ Kout,
                                double* __restrict__ ynew, double* __restrict__ err) {
-  const RayProblem P{F};
+  const RayProblem P{StaticBG{F}};
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     double yy[5], ff[5], yn[5], k6[5];
@@ -720,8 +838,9 @@ __global__ void attempt_kernel(Field F, int64_t n, const double* __restrict__ y,
   }
 }
 
+template <class BG>
 struct InitArgs {
-  Field F;
+  BG B;
   int64_t nray;
   const double* y0;
   double rtol, atol;
@@ -733,8 +852,9 @@ struct InitArgs {
   int64_t* summary;
 };
 
-__global__ void rk45_init_kernel(InitArgs a) {
-  const RayProblem P{a.F};
+template <class BG>
+__global__ void rk45_init_kernel(InitArgs<BG> a) {
+  const RayProblemT<BG> P{a.B};
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < a.nray;
        i += (int64_t)gridDim.x * blockDim.x) {
     double y[5], f[5];
@@ -762,8 +882,9 @@ __global__ void rk45_init_kernel(InitArgs a) {
   }
 }
 
+template <class BG>
 struct RunArgs {
-  Field F;
+  BG B;
   int64_t nray;
   double rtol, atol, min_step, cut_off;
   int32_t nt, it_begin, it_end;
@@ -798,8 +919,10 @@ using KStore = KShared<5>;
 #else
 using KStore = KRegs<5>;
 #endif
-__global__ void __launch_bounds__(256, RWRT_WAVES_PER_SIMD) rk45_run_kernel(RunArgs a) {
-  const RayProblem P{a.F};
+template <class BG>
+__global__ void __launch_bounds__(256, RWRT_WAVES_PER_SIMD) rk45_run_kernel(RunArgs<BG> a) {
+  using RayProblem = RayProblemT<BG>;
+  const RayProblem P{a.B};
   const int64_t nrows = a.it_end - a.it_begin;
 #if RWRT_K_IN_LDS
   __shared__ double kbuf[5 * 5 * 256];
@@ -859,7 +982,9 @@ __global__ void __launch_bounds__(256, RWRT_WAVES_PER_SIMD) rk45_run_kernel(RunA
     // inputs, same operations), so they are reused unless that evaluation was
     // masked (aux NaN) or y has changed since.
     double* y = L.y;
-    const bool have = !isnan(L.aux[2]);
+    // (a time-varying flow recomputes at t_bound: K6 was evaluated at t + h,
+    // which can differ from t_bound in the last bit)
+    const bool have = !BG::kTimeVarying && !isnan(L.aux[2]);
     double ug, vg, cos_c = kNaN;
     bool masked = fabs(y[1]) >= kHalfPi;
     if (!masked) {
@@ -876,7 +1001,7 @@ __global__ void __launch_bounds__(256, RWRT_WAVES_PER_SIMD) rk45_run_kernel(RunA
       ug = L.aux[0];
       vg = L.aux[1];
     } else {
-      ugvg_at(a.F, y[0], y[1], y[2], y[3], ug, vg);
+      ugvg_at(a.B, tb, y[0], y[1], y[2], y[3], ug, vg);
     }
     const double2 r0 = make_double2(y[0], y[1]), r1 = make_double2(y[2], y[3]);
     const double2 r2 = make_double2(y[4], ug), r3 = make_double2(vg, (double)nacc);
@@ -987,7 +1112,7 @@ __global__ void __launch_bounds__(256, RWRT_WAVES_PER_SIMD) rk4_run_kernel(Rk4Ar
 #pragma unroll
         for (int v = 0; v < 5; ++v) ys[v] = (s == 0) ? y[v] : y[v] + c * k[v];
         if (s > 0 && rhs_bad(ys)) held = true;
-        ray_rhs(a.F, ys, k);
+        ray_rhs(StaticBG{a.F}, 0.0, ys, k);
         const double wgt = (s == 1 || s == 2) ? 2.0 : 1.0;
 #pragma unroll
         for (int v = 0; v < 5; ++v) acc[v] = (s == 0) ? k[v] : acc[v] + wgt * k[v];
@@ -1010,7 +1135,7 @@ __global__ void __launch_bounds__(256, RWRT_WAVES_PER_SIMD) rk4_run_kernel(Rk4Ar
         for (int v = 0; v < 5; ++v) y[v] = kNaN;
       }
       double ug, vg;
-      ugvg_at(a.F, y[0], y[1], y[2], y[3], ug, vg);
+      ugvg_at(StaticBG{a.F}, 0.0, y[0], y[1], y[2], y[3], ug, vg);
       const double2 r0 = make_double2(y[0], y[1]), r1 = make_double2(y[2], y[3]);
       const double2 r2 = make_double2(y[4], ug), r3 = make_double2(vg, (double)nstep);
       // A held ray (masked first stage) or an all-NaN state repeats this row
@@ -1216,17 +1341,208 @@ int compute_units() {
   return cached;
 }
 
+template <class BG = StaticBG>
 int persistent_blocks() {
   static int cached = 0;
   if (cached) return cached;
   int dev = 0, ncu = 0, per = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 1024;
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) ncu = 256;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(rk45_run_kernel),
-                                                   256, 0) != hipSuccess || per < 1)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+          &per, reinterpret_cast<const void*>(rk45_run_kernel<BG>), 256, 0) != hipSuccess || per < 1)
     per = 1;
   cached = ncu * per;
   return cached;
+}
+
+// solver construction / ray loop launchers shared by the static and the
+// time-varying entry points
+template <class BG>
+rwrt_status launch_init(const BG& B, int64_t nray, const double* d_y0, const rwrt_params* p,
+                        double* d_state, int64_t* d_count, int32_t* d_nanrow, int32_t* d_live,
+                        int64_t* d_summary, void* stream) {
+  if (!p) return fail(RWRT_ERR_ARG, "params is NULL%s");
+  if (nray < 0 || nray > 0x7fffffffLL) return fail(RWRT_ERR_ARG, "nray out of range%s");
+  if (!d_y0 || !d_state || !d_count || !d_nanrow || !d_live || !d_summary)
+    return fail(RWRT_ERR_ARG, "NULL buffer to rwrt_rk45_init%s");
+  if (hipMemsetAsync(d_summary, 0, 2 * sizeof(int64_t), (hipStream_t)stream) != hipSuccess)
+    return check_launch("hipMemsetAsync(summary)");
+  if (nray == 0) return RWRT_OK;
+  InitArgs<BG> a{B, nray, d_y0, p->rtol, p->atol, p->nt, d_state, d_count, d_nanrow, d_live, d_summary};
+  hipLaunchKernelGGL(rk45_init_kernel<BG>, dim3(grid_for(nray, 256)), dim3(256), 0,
+                     (hipStream_t)stream, a);
+  return check_launch("rk45_init_kernel");
+}
+
+template <class BG>
+rwrt_status launch_run(const BG& B, int64_t nray, const rwrt_params* p, const double* d_tbound,
+                       int32_t it_begin, int32_t it_end, const int64_t* d_order, int64_t n_heavy,
+                       double* d_state, int64_t* d_count, int32_t* d_nanrow, double* d_out,
+                       int32_t* d_work, void* stream) {
+  if (!p) return fail(RWRT_ERR_ARG, "params is NULL%s");
+  if (nray < 0 || nray > 0x7fffffffLL) return fail(RWRT_ERR_ARG, "nray out of range%s");
+  if (it_begin < 1 || it_end > p->nt || it_begin >= it_end)
+    return fail(RWRT_ERR_ARG, "need 1 <= it_begin < it_end <= nt%s");
+  if (!d_tbound || !d_state || !d_count || !d_nanrow || !d_out || !d_work)
+    return fail(RWRT_ERR_ARG, "NULL buffer to rwrt_rk45_run%s");
+  if (reinterpret_cast<uintptr_t>(d_out) % 16 != 0)
+    return fail(RWRT_ERR_ARG, "output rows must be 16-byte aligned%s");
+  if (nray == 0) return RWRT_OK;
+  if (n_heavy < 0 || n_heavy > nray) return fail(RWRT_ERR_ARG, "n_heavy out of range%s");
+  if (hipMemsetAsync(d_work, 0, 2 * sizeof(int32_t), (hipStream_t)stream) != hipSuccess)
+    return check_launch("hipMemsetAsync(queue)");
+  int64_t blocks = persistent_blocks<BG>();
+  const int64_t need = (nray + 255) / 256;
+  if (blocks > need) blocks = need;
+  // one high-priority block per CU when at least two blocks share each CU
+  const int ncu = compute_units();
+  const int heavy_blocks = (d_order && n_heavy > 0 && blocks >= 2 * (int64_t)ncu) ? ncu : 0;
+  RunArgs<BG> a{B, nray, p->rtol, p->atol, p->min_step, p->cut_off, p->nt, it_begin, it_end,
+                d_tbound, d_order, d_state, d_count, d_nanrow, d_out, d_work,
+                heavy_blocks ? n_heavy : 0, heavy_blocks};
+  hipLaunchKernelGGL(rk45_run_kernel<BG>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
+  return check_launch("rk45_run_kernel");
+}
+
+// a time-varying background from the ABI description
+template <class T>
+rwrt_status make_varying(const rwrt_grid* g, const rwrt_background* b, VaryingBG<T>& B) {
+  Field F;
+  if (!b) return fail(RWRT_ERR_ARG, "background is NULL%s");
+  if (rwrt_status s = make_field(g, reinterpret_cast<const double*>(b->d_levels), F)) return s;
+  if (b->nlev < 1) return fail(RWRT_ERR_ARG, "background needs nlev >= 1%s");
+  if (!(b->dt > 0.0)) return fail(RWRT_ERR_ARG, "background level spacing dt must be > 0%s");
+  B.P = reinterpret_cast<const T*>(b->d_levels);
+  B.W = F.W;
+  B.H = F.H;
+  B.nlev = b->nlev;
+  B.lev_stride = (int64_t)F.W * F.H * kNF;
+  B.lon0 = F.lon0;
+  B.dlon = F.dlon;
+  B.lat0 = F.lat0;
+  B.dlat = F.dlat;
+  B.t0 = b->t0;
+  B.dt = b->dt;
+  return RWRT_OK;
+}
+
+// ---------------------------------------------------------------------------
+// BS.ready on the device (bs.py:264-279, 291-305, 318-372 / our bs.py):
+// three element passes over the (nlon, nlat) grid, every expression in the
+// reference's NumPy evaluation order.
+// ---------------------------------------------------------------------------
+struct ReadyArgs {
+  int nlon, nlat;
+  const float* u;      // [nlat][nlon] as read (file layout; BS keeps u.T)
+  const float* v;
+  const double* trig;  // [3][nlat]: np.cos(lat) (ucos), and at 1..nlat-2 np.cos / np.sin of lat[1:-1]
+  double dx2, dy2, dxx, dyy, dxy4, dx, dy;   // 2dx, 2dy, dx**2, dy**2, (4dx)dy, dx, dy
+  double* q;           // scratch [nlon][nlat] x 4: q, qxx, qyy, qxy (unsmoothed)
+  void* out;           // [nlon+1][nlat][12], double or float
+};
+
+__device__ __forceinline__ int wrapi(int i, int n) { return i < 0 ? i + n : (i >= n ? i - n : i); }
+__device__ __forceinline__ double U(const ReadyArgs& a, int i, int j) { return (double)a.u[(size_t)j * a.nlon + i]; }
+__device__ __forceinline__ double V(const ReadyArgs& a, int i, int j) { return (double)a.v[(size_t)j * a.nlon + i]; }
+
+// pass 1: absolute vorticity q (calc_absolute_vorticity, bs.py:264-279)
+__global__ void ready_q_kernel(ReadyArgs a) {
+  const int64_t n = (int64_t)a.nlon * a.nlat;
+  for (int64_t id = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; id < n;
+       id += (int64_t)gridDim.x * blockDim.x) {
+    const int i = (int)(id / a.nlat), j = (int)(id - (int64_t)i * a.nlat);
+    const int jj = j < 1 ? 1 : (j > a.nlat - 2 ? a.nlat - 2 : j);   // q[:,0]=q[:,1], q[:,-1]=q[:,-2]
+    const double vx = (V(a, wrapi(i + 1, a.nlon), jj) - V(a, wrapi(i - 1, a.nlon), jj)) / a.dx2;
+    const double ucp = U(a, i, jj + 1) * a.trig[jj + 1];
+    const double ucm = U(a, i, jj - 1) * a.trig[jj - 1];
+    const double uy = (ucp - ucm) / a.dy2;
+    a.q[(size_t)i * a.nlat + j] = (vx - uy) / a.trig[a.nlat + jj] +
+                                  ((2.0 * kOmega) * a.trig[2 * a.nlat + jj]) * kREarth;
+  }
+}
+
+// pass 2: unsmoothed qxx, qyy, qxy (gradient_xx / _yy / _xy)
+__global__ void ready_q2_kernel(ReadyArgs a) {
+  const int64_t n = (int64_t)a.nlon * a.nlat;
+  const double* q = a.q;
+  for (int64_t id = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; id < n;
+       id += (int64_t)gridDim.x * blockDim.x) {
+    const int i = (int)(id / a.nlat), j = (int)(id - (int64_t)i * a.nlat);
+    const int H = a.nlat;
+    const size_t ip = (size_t)wrapi(i + 1, a.nlon) * H, i0 = (size_t)i * H, im = (size_t)wrapi(i - 1, a.nlon) * H;
+    const int jj = j < 1 ? 1 : (j > H - 2 ? H - 2 : j);
+    const double qxx = ((q[ip + j] - 2.0 * q[i0 + j]) + q[im + j]) / a.dxx;
+    const double qyy = ((q[i0 + jj + 1] - 2.0 * q[i0 + jj]) + q[i0 + jj - 1]) / a.dyy;
+    const double qxy = (((q[ip + jj + 1] - q[ip + jj - 1]) - q[im + jj + 1]) + q[im + jj - 1]) / a.dxy4;
+    a.q[n + id] = qxx;
+    a.q[2 * n + id] = qyy;
+    a.q[3 * n + id] = qxy;
+  }
+}
+
+// smth9 (bs.py:291-305): f + convolve(f, w, 'constant') on [1:-2, 1:-2]
+__device__ __forceinline__ double smth9_at(const double* f, int nlon, int H, int i, int j) {
+  const double f0 = f[(size_t)i * H + j];
+  if (i < 1 || i > nlon - 3 || j < 1 || j > H - 3) return f0;
+  const double w[3][3] = {{0.0625, 0.125, 0.0625}, {0.125, -0.75, 0.125}, {0.0625, 0.125, 0.0625}};
+  double acc = 0.0;
+#pragma unroll
+  for (int da = 0; da < 3; ++da)
+#pragma unroll
+    for (int db = 0; db < 3; ++db) acc = acc + f[(size_t)(i + da - 1) * H + (j + db - 1)] * w[da][db];
+  return f0 + acc;
+}
+
+// gradient_y of column i of a field given by an accessor (bs.py gradient_y)
+template <class G>
+__device__ __forceinline__ double grad_y(const G& g, int j, int H, double dy2, double dy) {
+  if (j == 0) return (g(1) - g(0)) / dy;
+  if (j == H - 1) return (g(H - 1) - g(H - 2)) / dy;
+  return (g(j + 1) - g(j - 1)) / dy2;
+}
+
+// pass 3: the packed record of every grid point (+ the cyclic column)
+template <class T>
+__global__ void ready_pack_kernel(ReadyArgs a) {
+  const int H = a.nlat;
+  const int64_t n = (int64_t)(a.nlon + 1) * H, nq = (int64_t)a.nlon * H;
+  for (int64_t id = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; id < n;
+       id += (int64_t)gridDim.x * blockDim.x) {
+    const int ic = (int)(id / H), j = (int)(id - (int64_t)ic * H);
+    const int i = ic == a.nlon ? 0 : ic;                     // bs.py:370-372 cyclic copy
+    const int ip = wrapi(i + 1, a.nlon), im = wrapi(i - 1, a.nlon);
+    const double* q = a.q;
+    double r[12];
+    r[F_U] = U(a, i, j);
+    r[F_V] = V(a, i, j);
+    r[F_UX] = (U(a, ip, j) - U(a, im, j)) / a.dx2;
+    r[F_UY] = grad_y([&](int jj) { return U(a, i, jj); }, j, H, a.dy2, a.dy);
+    r[F_VX] = (V(a, ip, j) - V(a, im, j)) / a.dx2;
+    r[F_VY] = grad_y([&](int jj) { return V(a, i, jj); }, j, H, a.dy2, a.dy);
+    r[F_QX] = (q[(size_t)ip * H + j] - q[(size_t)im * H + j]) / a.dx2;
+    r[F_QY] = grad_y([&](int jj) { return q[(size_t)i * H + jj]; }, j, H, a.dy2, a.dy);
+    r[F_QXX] = smth9_at(q + nq, a.nlon, H, i, j);
+    r[F_QXY] = smth9_at(q + 3 * nq, a.nlon, H, i, j);
+    r[F_QYY] = smth9_at(q + 2 * nq, a.nlon, H, i, j);
+    r[F_PAD] = 0.0;
+    T* o = reinterpret_cast<T*>(a.out) + id * kNF;
+#pragma unroll
+    for (int k = 0; k < 12; ++k) o[k] = (T)r[k];
+  }
+}
+
+template <class BG>
+__global__ void rhs_bg_kernel(BG B, int64_t n, const double* __restrict__ t,
+                              const double* __restrict__ y, double* __restrict__ dydt) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    double yy[5], d[5];
+#pragma unroll
+    for (int v = 0; v < 5; ++v) yy[v] = y[v * n + i];
+    ray_rhs(B, t[i], yy, d);
+#pragma unroll
+    for (int v = 0; v < 5; ++v) dydt[v * n + i] = d[v];
+  }
 }
 
 }  // namespace rwrt
@@ -1309,17 +1625,8 @@ rwrt_status rwrt_rk45_init(const rwrt_grid* g, const double* d_packed, int64_t n
                            int64_t* d_summary, void* stream) {
   Field F;
   if (rwrt_status s = make_field(g, d_packed, F)) return s;
-  if (!p) return fail(RWRT_ERR_ARG, "params is NULL%s");
-  if (nray < 0 || nray > 0x7fffffffLL) return fail(RWRT_ERR_ARG, "nray out of range%s");
-  if (!d_y0 || !d_state || !d_count || !d_nanrow || !d_live || !d_summary)
-    return fail(RWRT_ERR_ARG, "NULL buffer to rwrt_rk45_init%s");
-  if (hipMemsetAsync(d_summary, 0, 2 * sizeof(int64_t), (hipStream_t)stream) != hipSuccess)
-    return check_launch("hipMemsetAsync(summary)");
-  if (nray == 0) return RWRT_OK;
-  InitArgs a{F, nray, d_y0, p->rtol, p->atol, p->nt, d_state, d_count, d_nanrow, d_live, d_summary};
-  hipLaunchKernelGGL(rk45_init_kernel, dim3(grid_for(nray, 256)), dim3(256), 0,
-                     (hipStream_t)stream, a);
-  return check_launch("rk45_init_kernel");
+  return launch_init(StaticBG{F}, nray, d_y0, p, d_state, d_count, d_nanrow, d_live, d_summary,
+                     stream);
 }
 
 rwrt_status rwrt_rk45_run(const rwrt_grid* g, const double* d_packed, int64_t nray,
@@ -1329,29 +1636,78 @@ rwrt_status rwrt_rk45_run(const rwrt_grid* g, const double* d_packed, int64_t nr
                           int32_t* d_work, void* stream) {
   Field F;
   if (rwrt_status s = make_field(g, d_packed, F)) return s;
-  if (!p) return fail(RWRT_ERR_ARG, "params is NULL%s");
-  if (nray < 0 || nray > 0x7fffffffLL) return fail(RWRT_ERR_ARG, "nray out of range%s");
-  if (it_begin < 1 || it_end > p->nt || it_begin >= it_end)
-    return fail(RWRT_ERR_ARG, "need 1 <= it_begin < it_end <= nt%s");
-  if (!d_tbound || !d_state || !d_count || !d_nanrow || !d_out || !d_work)
-    return fail(RWRT_ERR_ARG, "NULL buffer to rwrt_rk45_run%s");
-  if (reinterpret_cast<uintptr_t>(d_out) % 16 != 0)
-    return fail(RWRT_ERR_ARG, "output rows must be 16-byte aligned%s");
-  if (nray == 0) return RWRT_OK;
-  if (n_heavy < 0 || n_heavy > nray) return fail(RWRT_ERR_ARG, "n_heavy out of range%s");
-  if (hipMemsetAsync(d_work, 0, 2 * sizeof(int32_t), (hipStream_t)stream) != hipSuccess)
-    return check_launch("hipMemsetAsync(queue)");
-  int64_t blocks = persistent_blocks();
-  const int64_t need = (nray + 255) / 256;
-  if (blocks > need) blocks = need;
-  // one high-priority block per CU when at least two blocks share each CU
-  const int ncu = compute_units();
-  const int heavy_blocks = (d_order && n_heavy > 0 && blocks >= 2 * (int64_t)ncu) ? ncu : 0;
-  RunArgs a{F, nray, p->rtol, p->atol, p->min_step, p->cut_off, p->nt, it_begin, it_end,
-            d_tbound, d_order, d_state, d_count, d_nanrow, d_out, d_work,
-            heavy_blocks ? n_heavy : 0, heavy_blocks};
-  hipLaunchKernelGGL(rk45_run_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
-  return check_launch("rk45_run_kernel");
+  return launch_run(StaticBG{F}, nray, p, d_tbound, it_begin, it_end, d_order, n_heavy, d_state,
+                    d_count, d_nanrow, d_out, d_work, stream);
+}
+
+rwrt_status rwrt_rk45_init_tv(const rwrt_grid* g, const rwrt_background* b, int64_t nray,
+                              const double* d_y0, const rwrt_params* p, double* d_state,
+                              int64_t* d_count, int32_t* d_nanrow, int32_t* d_live,
+                              int64_t* d_summary, void* stream) {
+  if (b && b->fp32) {
+    VaryingBG<float> B;
+    if (rwrt_status s = make_varying(g, b, B)) return s;
+    return launch_init(B, nray, d_y0, p, d_state, d_count, d_nanrow, d_live, d_summary, stream);
+  }
+  VaryingBG<double> B;
+  if (rwrt_status s = make_varying(g, b, B)) return s;
+  return launch_init(B, nray, d_y0, p, d_state, d_count, d_nanrow, d_live, d_summary, stream);
+}
+
+rwrt_status rwrt_rk45_run_tv(const rwrt_grid* g, const rwrt_background* b, int64_t nray,
+                             const rwrt_params* p, const double* d_tbound, int32_t it_begin,
+                             int32_t it_end, const int64_t* d_order, int64_t n_heavy,
+                             double* d_state, int64_t* d_count, int32_t* d_nanrow, double* d_out,
+                             int32_t* d_work, void* stream) {
+  if (b && b->fp32) {
+    VaryingBG<float> B;
+    if (rwrt_status s = make_varying(g, b, B)) return s;
+    return launch_run(B, nray, p, d_tbound, it_begin, it_end, d_order, n_heavy, d_state, d_count,
+                      d_nanrow, d_out, d_work, stream);
+  }
+  VaryingBG<double> B;
+  if (rwrt_status s = make_varying(g, b, B)) return s;
+  return launch_run(B, nray, p, d_tbound, it_begin, it_end, d_order, n_heavy, d_state, d_count,
+                    d_nanrow, d_out, d_work, stream);
+}
+
+rwrt_status rwrt_rhs_tv(const rwrt_grid* g, const rwrt_background* b, int64_t n,
+                        const double* d_t, const double* d_y, double* d_dydt, void* stream) {
+  if (n < 0 || !d_t || !d_y || !d_dydt) return fail(RWRT_ERR_ARG, "bad rwrt_rhs_tv arguments%s");
+  if (n == 0) return RWRT_OK;
+  const dim3 grid(grid_for(n, 256)), block(256);
+  if (b && b->fp32) {
+    VaryingBG<float> B;
+    if (rwrt_status s = make_varying(g, b, B)) return s;
+    hipLaunchKernelGGL(rhs_bg_kernel<VaryingBG<float>>, grid, block, 0, (hipStream_t)stream, B, n,
+                       d_t, d_y, d_dydt);
+  } else {
+    VaryingBG<double> B;
+    if (rwrt_status s = make_varying(g, b, B)) return s;
+    hipLaunchKernelGGL(rhs_bg_kernel<VaryingBG<double>>, grid, block, 0, (hipStream_t)stream, B, n,
+                       d_t, d_y, d_dydt);
+  }
+  return check_launch("rhs_bg_kernel");
+}
+
+rwrt_status rwrt_bs_ready(int32_t nlon, int32_t nlat, const float* d_u, const float* d_v,
+                          const double* d_trig, double dx, double dy, double* d_scratch,
+                          void* d_packed, int32_t fp32, void* stream) {
+  if (nlon < 3 || nlat < 4) return fail(RWRT_ERR_ARG, "bs_ready needs nlon >= 3 and nlat >= 4%s");
+  if (!d_u || !d_v || !d_trig || !d_scratch || !d_packed) return fail(RWRT_ERR_ARG, "NULL buffer to rwrt_bs_ready%s");
+  if (reinterpret_cast<uintptr_t>(d_packed) % 16 != 0)
+    return fail(RWRT_ERR_ARG, "packed fields must be 16-byte aligned%s");
+  ReadyArgs a{nlon, nlat, d_u, d_v, d_trig, 2.0 * dx, 2.0 * dy, dx * dx, dy * dy, (4.0 * dx) * dy,
+              dx, dy, d_scratch, d_packed};
+  const int64_t n = (int64_t)nlon * nlat, n1 = (int64_t)(nlon + 1) * nlat;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(ready_q_kernel, dim3(grid_for(n, 256)), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(ready_q2_kernel, dim3(grid_for(n, 256)), dim3(256), 0, st, a);
+  if (fp32)
+    hipLaunchKernelGGL(ready_pack_kernel<float>, dim3(grid_for(n1, 256)), dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL(ready_pack_kernel<double>, dim3(grid_for(n1, 256)), dim3(256), 0, st, a);
+  return check_launch("bs_ready kernels");
 }
 
 rwrt_status rwrt_rk4_run(const rwrt_grid* g, const double* d_packed, int64_t nray,
@@ -1374,7 +1730,7 @@ rwrt_status rwrt_rk4_run(const rwrt_grid* g, const double* d_packed, int64_t nra
     return check_launch("hipMemsetAsync(queue)");
   Rk4Args a{F, nray, p->tstep, p->cut_off, p->nt, it_begin, it_end, d_order, d_state, d_count,
             d_nanrow, d_out, d_work};
-  int64_t blocks = persistent_blocks();
+  int64_t blocks = persistent_blocks<StaticBG>();
   const int64_t need = (nray + 255) / 256;
   if (blocks > need) blocks = need;
   hipLaunchKernelGGL(rk4_run_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);

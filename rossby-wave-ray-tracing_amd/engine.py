@@ -67,9 +67,51 @@ class RayEngine:
         H.check(H.load().rwrt_pack_fields(self.grid, H.dptr(f), H.dptr(self.packed), H.stream()))
         self.work = torch.zeros(4, dtype=torch.int32, device=self.device)
 
+    bg = None   # rwrt_background of a time-varying state (None: the reference's static state)
+
     @classmethod
     def from_bs(cls, bs, device=None):
         return cls(bs.fields, bs.lon, bs.lat, device)
+
+    @classmethod
+    def from_levels(cls, levels):
+        """Engine over a ``levels.Levels`` basic state.  One fp64 level is the
+        reference's static state (same kernels, same bits); otherwise the
+        time-varying kernels (``rwrt_rk45_*_tv``) run."""
+        self = cls.__new__(cls)
+        self.device = levels.device
+        self.grid = levels.grid
+        self.levels = levels
+        self.work = torch.zeros(4, dtype=torch.int32, device=self.device)
+        if levels.nlev == 1 and not levels.fp32:
+            self.packed = levels.packed[0]
+            self.bg = None
+        else:
+            self.packed = None
+            self.bg = levels.background()
+        return self
+
+    @classmethod
+    def from_packed(cls, packed, lon, lat):
+        """Engine over an already packed ``[nlon+1, nlat, 12]`` fp64 state (e.g.
+        from ``rwrt_bs_ready``)."""
+        self = cls.__new__(cls)
+        self.device = packed.device
+        self.grid = grid_of(lon, lat, packed.shape[0])
+        self.packed = packed.contiguous()
+        self.work = torch.zeros(4, dtype=torch.int32, device=self.device)
+        return self
+
+    def rhs_t(self, t, y):
+        """The time-varying RHS at per-point times ``t[n]`` for ``y[5, n]``."""
+        if self.bg is None:
+            return self.rhs(y)
+        y = torch.as_tensor(y, dtype=F64, device=self.device).contiguous()
+        t = torch.as_tensor(t, dtype=F64, device=self.device).contiguous()
+        out = torch.empty_like(y)
+        H.check(H.load().rwrt_rhs_tv(self.grid, ctypes_ref(self.bg), y.shape[1], H.dptr(t),
+                                     H.dptr(y), H.dptr(out), H.stream()))
+        return out
 
     # ------------------------------------------------------------------ T0/T1
     def mercator_point(self, lon, lat):
@@ -138,7 +180,8 @@ class RayEngine:
             rows = torch.empty((7, 3, ns, nz), dtype=F64, device=self.device)
         if info is None:
             info = torch.zeros(1, dtype=torch.int32, device=self.device)
-        H.check(H.load().rwrt_ray_initial(self.grid, H.dptr(self.packed), ns, H.dptr(src[0]),
+        packed = self.packed if self.bg is None else self.levels.level0_f64   # the t = 0 state
+        H.check(H.load().rwrt_ray_initial(self.grid, H.dptr(packed), ns, H.dptr(src[0]),
                                           H.dptr(src[1]), H.dptr(src[2]), nz, H.dptr(zc),
                                           H.dptr(rows), H.dptr(info), H.stream()))
         return rows, info
@@ -179,10 +222,14 @@ class RayEngine:
             live=torch.empty(nray, dtype=torch.int32, device=self.device),
             summary=torch.zeros(2, dtype=torch.int64, device=self.device),
             nray=nray)
-        H.check(H.load().rwrt_rk45_init(self.grid, H.dptr(self.packed), nray, H.dptr(y0),
-                                        ctypes_ref(p), H.dptr(st["state"]), H.dptr(st["count"]),
-                                        H.dptr(st["nanrow"]), H.dptr(st["live"]),
-                                        H.dptr(st["summary"]), H.stream()))
+        lib = H.load()
+        if self.bg is None:
+            fn, bg = lib.rwrt_rk45_init, H.dptr(self.packed)
+        else:
+            fn, bg = lib.rwrt_rk45_init_tv, ctypes_ref(self.bg)
+        H.check(fn(self.grid, bg, nray, H.dptr(y0), ctypes_ref(p), H.dptr(st["state"]),
+                   H.dptr(st["count"]), H.dptr(st["nanrow"]), H.dptr(st["live"]),
+                   H.dptr(st["summary"]), H.stream()))
         return st
 
     @staticmethod
@@ -210,8 +257,13 @@ class RayEngine:
 
     def run(self, st, p, tbound, it_begin, it_end, out, order=None, n_heavy=0):
         """Rows ``[it_begin, it_end)`` into ``out[nray, it_end-it_begin, 8]`` (async)."""
-        H.check(H.load().rwrt_rk45_run(
-            self.grid, H.dptr(self.packed), st["nray"], ctypes_ref(p), H.dptr(tbound, F64),
+        lib = H.load()
+        if self.bg is None:
+            fn, bg = lib.rwrt_rk45_run, H.dptr(self.packed)
+        else:
+            fn, bg = lib.rwrt_rk45_run_tv, ctypes_ref(self.bg)
+        H.check(fn(
+            self.grid, bg, st["nray"], ctypes_ref(p), H.dptr(tbound, F64),
             int(it_begin), int(it_end), H.dptr(order, torch.int64), int(n_heavy),
             H.dptr(st["state"]),
             H.dptr(st["count"]), H.dptr(st["nanrow"]), H.dptr(out, F64), H.dptr(self.work),
@@ -225,6 +277,8 @@ class RayEngine:
         ``RunResult.nacc`` count RK4 steps taken, ``nrej`` steps held because a
         stage input was masked (the ray keeps its state, wr.py:609-618).
         """
+        if self.bg is not None:
+            raise NotImplementedError("the RK4 loop runs on the reference's static basic state")
         p = self.params(nt, tstep, cut_off=cut_off, cut_rad=cut_rad)
         y0 = torch.as_tensor(y0, dtype=F64, device=self.device).contiguous()
         nray = y0.shape[1]

@@ -17,7 +17,7 @@ them from netCDF: ``u, v`` float32 ``(nlat, nlon)``, ``lat, lon`` float32.
 """
 import numpy as np
 
-__all__ = ["background", "SeedConfig", "CONFIGS", "config"]
+__all__ = ["background", "background_level", "SeedConfig", "CONFIGS", "config"]
 
 
 def background(kind="zonal", res=2.5):
@@ -37,6 +37,32 @@ def background(kind="zonal", res=2.5):
         v = 4.0 * np.sin(3.0 * np.deg2rad(lam)) * coslat ** 2
     elif kind != "zonal":
         raise ValueError(f"unknown background kind {kind!r}")
+    return dict(u=u.astype(np.float32), v=v.astype(np.float32), lat=lat, lon=lon)
+
+
+def _jets(phi_deg):
+    return (45.0 * np.exp(-((phi_deg - 32.0) / 10.0) ** 2)
+            + 28.0 * np.exp(-((phi_deg + 45.0) / 12.0) ** 2)
+            - 5.0 * np.exp(-(phi_deg / 10.0) ** 2))
+
+
+def background_level(j, res=2.5, dt_hours=6.0, seed=0, nlev_max=4096):
+    """Level ``j`` (valid at ``j * dt_hours``) of the time-varying C5 background
+    (SURVEY.md §8(d)): the non-zonal jet of ``background('nonzonal')`` plus a
+    travelling wave-4 that moves east at 10 deg/day with a random-walk phase
+    (``numpy.random.default_rng(seed)``), and a westward-drifting wave-3 in V.
+    Returns ``dict(u, v, lat, lon)`` like ``background``."""
+    lat = np.arange(-90.0, 90.0 + res / 2, res).astype(np.float32)
+    lon = np.arange(0.0, 360.0, res).astype(np.float32)
+    phi = lat.astype(np.float64)[:, None]
+    lam = np.deg2rad(lon.astype(np.float64))[None, :]
+    t_days = j * dt_hours / 24.0
+    phase = np.cumsum(np.random.default_rng(seed).normal(0.0, 0.08, size=nlev_max))[j]
+    coslat = np.cos(np.deg2rad(phi))
+    wave4 = np.cos(4.0 * (lam - np.deg2rad(10.0) * t_days) + phase)
+    u = _jets(phi) * coslat * (1.0 + 0.3 * np.cos(lam - np.deg2rad(140.0)) + 0.15 * wave4)
+    v = (4.0 * np.sin(3.0 * lam + np.deg2rad(5.0) * t_days)
+         + 2.0 * np.sin(4.0 * (lam - np.deg2rad(10.0) * t_days) + phase)) * coslat ** 2
     return dict(u=u.astype(np.float32), v=v.astype(np.float32), lat=lat, lon=lon)
 
 
@@ -93,7 +119,13 @@ CONFIGS = {
                zwn=[3.0, 4.0, 5.0, 6.0]),
     "C3": dict(SW_lon=0.0, SW_lat=-88.0, dlon=2, dlat=2, nnx=180, nny=89,
                zwn=[float(k) for k in range(1, 11)]),
+    # C5 (BASELINE configs[4]): 1-degree global seeds x k = 1..10 on the 0.25-degree
+    # time-varying background; x 2 periods {stationary, 10 d} = 3.87 M ray slots
+    "C5": dict(SW_lon=0.0, SW_lat=-89.0, dlon=1, dlat=1, nnx=360, nny=179,
+               zwn=[float(k) for k in range(1, 11)]),
 }
+
+C5_PERIODS_DAYS = [None, 10.0]
 
 C3_PERIODS_DAYS = [None, 50.0, 30.0, 20.0, 10.0]   # None = stationary (freq 0)
 

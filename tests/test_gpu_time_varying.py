@@ -1,0 +1,149 @@
+"""GPU parity of the time-varying basic-state path.
+
+* ``rwrt_bs_ready`` (the reference's ``BS.ready`` on the device) is bit-identical
+  to the host ``BS.fields`` -- 2.5-degree backgrounds and a C5 level at 1 and
+  0.25 degrees; the fp32 storage is the host fields rounded once.
+* The time-varying RHS and ray loop (``rwrt_rhs_tv``, ``rwrt_rk45_*_tv``) against
+  the oracle's restatement of the extension (the reference has no time-varying
+  mode, so this is the parity bar; tests/test_time_varying_oracle.py pins the
+  restatement to the reference's RHS at the level times).  Tolerances are the
+  static path's: RHS within 16 ulp / 1e-14 of scale, trajectories within 1e-6
+  rad after 2 h and within 3x the reference's non-zonal 1-ulp noise floor
+  after 1 day.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import rwrt_oracle as O
+import synthetic as S
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+HOT = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 11]
+DT = 6 * 3600.0
+
+
+def host_fields(b):
+    from bs import BS
+    bs = BS(len(b["lon"]), len(b["lat"]))
+    bs.load_arrays(**b)
+    bs.ready(xcyclic=True)
+    return bs.fields
+
+
+def same_bits(a, b):
+    return a.shape == b.shape and np.array_equal(a, b, equal_nan=True)
+
+
+@pytest.mark.parametrize("case", ["zonal", "nonzonal", "c5_1deg", "c5_025deg"])
+def test_bs_ready_gpu_bitwise(case):
+    from levels import Levels
+    if case in ("zonal", "nonzonal"):
+        b = S.background(case)
+    else:
+        b = S.background_level(7, res=1.0 if case == "c5_1deg" else 0.25)
+    ref = host_fields(b)[..., HOT]
+    for fp32 in (False, True):
+        lv = Levels(b["lat"], b["lon"], 1, fp32=fp32)
+        lv.set_level(0, b["u"], b["v"])
+        dev = lv.packed[0].cpu().numpy()
+        want = ref.astype(np.float32) if fp32 else ref
+        assert same_bits(dev[..., :11], want), (case, fp32)
+        assert not dev[..., 11].any()
+        if fp32:
+            assert same_bits(lv.level0_f64.cpu().numpy()[..., :11], ref)
+
+
+_TV = {}
+
+
+def tv(fp32, nlev=5):
+    key = (fp32, nlev)
+    if key not in _TV:
+        from engine import RayEngine
+        from levels import Levels
+        bl = [S.background_level(j) for j in range(nlev)]
+        lv = Levels(bl[0]["lat"], bl[0]["lon"], nlev, t0=0.0, dt=DT, fp32=fp32)
+        for j, b in enumerate(bl):
+            lv.set_level(j, b["u"], b["v"])
+        ob = O.TimeVaryingBackground([O.Background(**b) for b in bl], 0.0, DT, fp32=fp32)
+        _TV[key] = (RayEngine.from_levels(lv), ob, O.Background(**bl[0]))
+    return _TV[key]
+
+
+def ulps(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    assert np.array_equal(np.isnan(a), np.isnan(b))
+    a, b = np.nan_to_num(a), np.nan_to_num(b)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        d = np.abs(a - b) / np.spacing(np.maximum(np.abs(a), np.abs(b)))
+    d[a == b] = 0
+    return d
+
+
+@pytest.mark.parametrize("fp32", [False, True])
+def test_rhs_tv_vs_oracle(fp32):
+    eng, ob, _ = tv(fp32)
+    rng = np.random.default_rng(11)
+    n = 4096
+    y = np.empty((5, n))
+    y[0] = rng.uniform(-1.0, 8.0, n)
+    y[1] = rng.uniform(-1.56, 1.56, n)
+    y[2] = rng.integers(1, 8, n).astype(float)
+    y[3] = rng.uniform(-8, 8, n)
+    y[4] = rng.uniform(0.5, 2.0, n)
+    t = rng.uniform(-3600.0, 4 * DT + 3600.0, n)
+    t[:64] = np.arange(64) % 5 * DT           # exactly at level times
+    out = eng.rhs_t(t, y).cpu().numpy()
+    ref = O.rhs(ob, y, t)[0]
+    for v in range(5):
+        scale = np.nanmax(np.abs(ref[v])) or 1.0
+        d = ulps(out[v], ref[v])
+        bad = (d > 16) & (np.abs(out[v] - ref[v]) > 1e-14 * scale)
+        assert not bad.any(), (v, np.nanmax(d))
+
+
+@pytest.mark.parametrize("fp32", [False, True])
+def test_tv_trajectories_vs_oracle(fp32):
+    eng, ob, ob0 = tv(fp32)
+    cfg = S.config("C2")
+    slon, slat = O.source_matrix(cfg.SW_lon, cfg.SW_lat, cfg.dlon, cfg.dlat, cfg.nnx, cfg.nny)
+    rows = eng.initial_rows(slon, slat, cfg.zwn, cfg.freq).cpu().numpy()
+    with np.errstate(all="ignore"):
+        ref_rows = np.array(O.ray_initial(ob0, slon, slat, cfg.zwn, cfg.freq))
+    assert np.array_equal(rows, ref_rows, equal_nan=True)    # init reads level 0 (fp64)
+    y0 = rows[:5].reshape(5, -1)
+    nt = 13
+    got = {}
+    res = eng.integrate(torch.as_tensor(y0), nt, 7200.0, ttotal=(nt - 1) * 7200.0,
+                        sink=lambda a, b, o: got.__setitem__(a, o.cpu().numpy().copy()))
+    hist = np.concatenate([got[k] for k in sorted(got)], axis=1)       # rows 1..nt-1
+    with np.errstate(all="ignore"):
+        ref, nacc, _, st = O.ray_run(ob, y0.copy(), nt, 7200.0)
+    assert st == 0
+    floor = json.load(open(os.path.join(GOLDEN, "noise_floor_C2_nonzonal.json")))["1d"]
+    for row in (1, 12):
+        a, b = hist[:, row - 1, :2], ref[:2, row].T
+        assert np.sum(np.isnan(a[:, 0]) != np.isnan(b[:, 0])) <= (0 if row == 1 else max(3, len(a) // 100))
+        ok = ~np.isnan(a).any(1) & ~np.isnan(b).any(1)
+        d = np.max(np.abs(a[ok] - b[ok]), axis=1)
+        if row == 1:
+            assert d.max() <= 1e-6, d.max()
+        else:
+            assert np.percentile(d, 99) <= 3 * floor["p99"], np.percentile(d, 99)
+            assert d.max() <= 3 * floor["max"], d.max()
+        if row == 1:
+            # group velocity at the row time (wr.py:856-865 on the row's state)
+            ga, gb = hist[ok, row - 1, 5:7], ref[5:7, row][:, ok].T
+            assert np.array_equal(np.isnan(ga), np.isnan(gb))
+            fin = ~np.isnan(ga).any(1)
+            dug = np.abs(ga[fin] - gb[fin]).max(1)
+            assert np.percentile(dug, 99) <= 1e-9 and dug.max() <= 1e-4 + 1e5 * d.max(), \
+                (np.percentile(dug, 99), dug.max(), d.max())
+    n_gpu = int(res.nacc.sum().item())
+    assert abs(n_gpu - int(nacc.sum())) <= 0.01 * int(nacc.sum())
