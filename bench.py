@@ -327,7 +327,12 @@ def main_c5(args, dist, rank, world, dev):
     y0 = make_y0()
     nslot = y0.shape[1]
     n_live = int((~torch.isnan(y0.sum(0))).sum().item())
-    chunk = args.chunk or 12          # one day per launch: <= 5 levels in flight (L2/MALL window)
+    # rows per launch (measured, profiles/r1/c5/chunk_sweep.txt): fp64 levels want a
+    # short time window (4 days: 17 levels in flight), fp32 levels the longest
+    # launches the output buffer allows (fewer launch tails beat locality)
+    free = torch.cuda.mem_get_info(dev)[0]
+    cap = max(1, min(nt - 1, int(0.8 * free) // (nslot * 64)))
+    chunk = min(args.chunk or (cap if lv.fp32 else 48), cap)
     out = torch.empty((nslot, min(chunk, nt - 1), 8), dtype=torch.float64, device=dev)
 
     def one_step(events=None):
