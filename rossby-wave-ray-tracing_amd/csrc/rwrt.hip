@@ -123,14 +123,54 @@ __device__ __forceinline__ double py_mod_2pi(double a) { return py_mod(a, kTwoPi
 // identity, except that a remainder that rounded up to 2 pi itself becomes +0.
 __device__ __forceinline__ double py_mod_2pi_again(double m) { return (m >= kTwoPi) ? 0.0 : m; }
 
-// np.floor(x).astype('int32') on x86-64: out-of-range and NaN give INT32_MIN.
-__device__ __forceinline__ int64_t floor_i32(double x) {
-  double f = floor(x);
-  if (!(f >= -2147483648.0 && f <= 2147483647.0)) return -2147483648LL;
-  return (int64_t)f;
+// np.floor(x).astype('int32') on x86-64 (cvttsd2si): out-of-range and NaN give
+// INT32_MIN.  v_cvt_i32_f64 saturates (INT32_MIN below the range, as x86) and
+// maps NaN to 0; above the range x86's INT32_MIN is restored.  (NaN -> 0 only
+// moves the x1/y1 corner of a lookup whose weights are NaN: same NaN result.)
+__device__ __forceinline__ int floor_i32(double x) {
+  const double f = floor(x);
+  const int i = __double2int_rz(f);
+  return (f > 2147483647.0) ? INT32_MIN : i;
 }
-__device__ __forceinline__ int clip(int64_t v, int hi) {
-  return (int)(v < 0 ? 0 : (v > hi ? hi : v));
+// x0 + 1 on an int32 array: wraps (NumPy integer arithmetic is modular)
+__device__ __forceinline__ int inc_i32(int v) { return (int)((unsigned)v + 1u); }
+// np.clip(v, 0, hi) -> v_med3_i32
+__device__ __forceinline__ int clip(int v, int hi) { return ::max(0, ::min(v, hi)); }
+
+// a / b with the reciprocal rb of b precomputed by recip_hw(b): the same
+// operations as the compiler's IEEE f64 division (v_div_scale, v_rcp_f64, two
+// Newton steps, q = a*r, rem = fma(-b, q, a), q' = fma(rem, r, q),
+// v_div_fixup) minus the scaling and special-case steps, which are the
+// identity when nothing is near the exponent limits: b in [2^-100, 2^100]
+// (else recip_hw returns 0 and every quotient takes the IEEE division), a in
+// {0} U [2^-900, 2^600] (else, or non-finite, the IEEE division).  The sign of
+// a zero quotient comes from q = a * r.  Bit-identical to a / b
+// (tests/test_gpu_parity.py::test_device_math_exactness).
+__device__ __forceinline__ double recip_hw(double b) {
+  const double ab = fabs(b);
+  double r = __builtin_amdgcn_rcp(b);
+  double e = fma(-b, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-b, r, 1.0);
+  r = fma(r, e, r);
+  return (ab >= 0x1p-100 && ab <= 0x1p100) ? r : 0.0;
+}
+__device__ __forceinline__ double div_hw(double a, double b, double rb) {
+  const double q = a * rb;
+  const double rem = fma(-b, q, a);
+  double r = copysign(fma(rem, rb, q), q);
+  const double aa = fabs(a);
+  const bool bad = !(aa < 0x1p600) | ((aa < 0x1p-900) & (aa != 0.0)) | (rb == 0.0);
+  if (bad) {
+    asm volatile("");   // keep the IEEE division on its (rarely taken) branch
+    r = a / b;
+  }
+  return r;
+}
+// x / c for a wave-uniform c: the reciprocal is loop-invariant (hoisted to
+// the kernel entry)
+__device__ __forceinline__ double div_uniform(double x, double c) {
+  return div_hw(x, c, recip_hw(c));
 }
 
 // ---------------------------------------------------------------------------
@@ -146,7 +186,7 @@ __constant__ int kRefIndex[11] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 11};
 #define RWRT_STAGE_BARRIER 0
 #endif
 #ifndef RWRT_INTERP_GROUP
-#define RWRT_INTERP_GROUP 6   // records (of 2 fields) per load group, divides 6
+#define RWRT_INTERP_GROUP 2   // records (of 2 fields) per load group, divides 6
 #endif
 
 struct Field {
@@ -163,26 +203,32 @@ struct Corners {
   const double* c;  // F[x0, y0]
   const double* d;  // F[x1, y0]
   double wa, wb, wc, wd;
+  unsigned key_x, key_y;   // x0 | x1 << 16, y0 | y1 << 16 (W, H < 2^16)
 };
 
 __device__ __forceinline__ Corners corners(const Field& F, double lon, double lat) {
   // lon arrives already reduced once (bs.py:519); interpolation.py:80 reduces again.
   const double lons = py_mod_2pi_again(lon);
-  const double x = (lons - F.lon0) / F.dlon;
-  const double y = (lat - F.lat0) / F.dlat;
-  const int64_t ix = floor_i32(x), iy = floor_i32(y);
-  const int x0 = clip(ix, F.W - 1), x1 = clip(ix + 1, F.W - 1);
-  const int y0 = clip(iy, F.H - 1), y1 = clip(iy + 1, F.H - 1);
+  const double x = div_uniform(lons - F.lon0, F.dlon);
+  const double y = div_uniform(lat - F.lat0, F.dlat);
+  const int ix = floor_i32(x), iy = floor_i32(y);
+  const int x0 = clip(ix, F.W - 1), x1 = clip(inc_i32(ix), F.W - 1);
+  const int y0 = clip(iy, F.H - 1), y1 = clip(inc_i32(iy), F.H - 1);
   const double sx = x - (double)x0, sy = y - (double)y0;
+  // 32-bit element offsets (a packed state holds < 2^31 doubles; checked on the host)
+  // (W, H < 2^24: 24-bit multiplies)
+  const unsigned c0 = __umul24(x0, F.H), c1 = __umul24(x1, F.H);
   Corners k;
-  k.a = F.P + ((size_t)x0 * F.H + y1) * kNF;
-  k.b = F.P + ((size_t)x1 * F.H + y1) * kNF;
-  k.c = F.P + ((size_t)x0 * F.H + y0) * kNF;
-  k.d = F.P + ((size_t)x1 * F.H + y0) * kNF;
+  k.a = F.P + __umul24(c0 + y1, kNF);
+  k.b = F.P + __umul24(c1 + y1, kNF);
+  k.c = F.P + __umul24(c0 + y0, kNF);
+  k.d = F.P + __umul24(c1 + y0, kNF);
   k.wa = (1.0 - sx) * sy;
   k.wb = sx * sy;
   k.wc = (1.0 - sx) * (1.0 - sy);
   k.wd = sx * (1.0 - sy);
+  k.key_x = (unsigned)x0 | ((unsigned)x1 << 16);
+  k.key_y = (unsigned)y0 | ((unsigned)y1 << 16);
   return k;
 }
 
@@ -262,6 +308,73 @@ struct StaticBG {
   }
 };
 
+// StaticBG with a per-lane cache of the last cell's four corner records (the
+// 11 hot fields of F[x0,y1], F[x1,y1], F[x0,y0], F[x1,y0]) in LDS.  The six
+// stage evaluations of an attempt lie within a fraction of a 2.5-degree cell
+// (C3: ~0.3 cell changes per 2-h interval against ~10 RHS evaluations), so a
+// lookup is usually 44 conflict-free LDS reads instead of 24 scattered 16-B
+// global gathers.  Same values, same blend: results are unchanged.
+#ifndef RWRT_CELL_CACHE
+#define RWRT_CELL_CACHE 1
+#endif
+[[maybe_unused]] constexpr int kCacheVals = 44;   // 4 corners x 11 fields
+struct CachedStaticBG {
+  static constexpr bool kTimeVarying = false;
+  Field F;
+  double* c;                      // this lane's slice: (corner j, field q) at c[(j * 11 + q) * 256]
+  mutable unsigned key_x, key_y;  // cell held in the slice (~0u: none)
+
+  __device__ __forceinline__ double& at(int j, int q) const { return c[(j * 11 + q) * 256]; }
+  __device__ __forceinline__ void interp11(double lon, double lat, double, double g[11]) const {
+    if (!(fabs(lat) <= kHalfPi)) {
+#pragma unroll
+      for (int i = 0; i < 11; ++i) g[i] = kNaN;
+      return;
+    }
+    const Corners k = corners(F, py_mod_2pi(lon), lat);
+    if (k.key_x != key_x || k.key_y != key_y) {   // miss: gather the cell once
+      const double* src[4] = {k.a, k.b, k.c, k.d};
+      double2 v[4][6];   // all 24 gathers in flight before the LDS writes
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int q = 0; q < 6; ++q) v[j][q] = reinterpret_cast<const double2*>(src[j])[q];
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int q = 0; q < 11; ++q) at(j, q) = (q & 1) ? v[j][q >> 1].y : v[j][q >> 1].x;
+      key_x = k.key_x;
+      key_y = k.key_y;
+    }
+#pragma unroll
+    for (int q = 0; q < 11; ++q) g[q] = blend(k, at(0, q), at(1, q), at(2, q), at(3, q));
+  }
+  __device__ __forceinline__ void interp4(double lon, double lat, double, double& fu, double& fv,
+                                          double& fqx, double& fqy) const {
+    rwrt::interp4(F, py_mod_2pi(lon), lat, fu, fv, fqx, fqy);
+  }
+};
+
+// The background a persistent lane integrates with: the cached lookup for the
+// static state (kernel-owned LDS slice), the plain one otherwise.
+template <class BG>
+struct LaneBG {
+  using type = BG;
+  static constexpr int kLds = 0;
+  __device__ static BG make(const BG& B, double*) { return B; }
+};
+#if RWRT_CELL_CACHE
+template <>
+struct LaneBG<StaticBG> {
+  using type = CachedStaticBG;
+  static constexpr int kLds = kCacheVals;
+  __device__ static CachedStaticBG make(const StaticBG& B, double* slice) {
+    return CachedStaticBG{B.F, slice, ~0u, ~0u};
+  }
+};
+#endif
+
 template <class T>
 struct VaryingBG {
   static constexpr bool kTimeVarying = true;
@@ -271,18 +384,19 @@ struct VaryingBG {
   double lon0, dlon, lat0, dlat, t0, dt;
 
   // cell corners and weights: the arithmetic of corners() (interpolation.py:77-135)
-  __device__ __forceinline__ void cell(double lon, double lat, size_t o[4], double w[4]) const {
+  __device__ __forceinline__ void cell(double lon, double lat, unsigned o[4], double w[4]) const {
     const double lons = py_mod_2pi_again(py_mod_2pi(lon));
-    const double x = (lons - lon0) / dlon;
-    const double y = (lat - lat0) / dlat;
-    const int64_t ix = floor_i32(x), iy = floor_i32(y);
-    const int x0 = clip(ix, W - 1), x1 = clip(ix + 1, W - 1);
-    const int y0 = clip(iy, H - 1), y1 = clip(iy + 1, H - 1);
+    const double x = div_uniform(lons - lon0, dlon);
+    const double y = div_uniform(lat - lat0, dlat);
+    const int ix = floor_i32(x), iy = floor_i32(y);
+    const int x0 = clip(ix, W - 1), x1 = clip(inc_i32(ix), W - 1);
+    const int y0 = clip(iy, H - 1), y1 = clip(inc_i32(iy), H - 1);
     const double sx = x - (double)x0, sy = y - (double)y0;
-    o[0] = ((size_t)x0 * H + y1) * kNF;   // a = F[x0, y1]
-    o[1] = ((size_t)x1 * H + y1) * kNF;   // b = F[x1, y1]
-    o[2] = ((size_t)x0 * H + y0) * kNF;   // c = F[x0, y0]
-    o[3] = ((size_t)x1 * H + y0) * kNF;   // d = F[x1, y0]
+    const unsigned c0 = __umul24(x0, H), c1 = __umul24(x1, H);
+    o[0] = __umul24(c0 + y1, kNF);   // a = F[x0, y1]
+    o[1] = __umul24(c1 + y1, kNF);   // b = F[x1, y1]
+    o[2] = __umul24(c0 + y0, kNF);   // c = F[x0, y0]
+    o[3] = __umul24(c1 + y0, kNF);   // d = F[x1, y0]
     w[0] = (1.0 - sx) * sy;
     w[1] = sx * sy;
     w[2] = (1.0 - sx) * (1.0 - sy);
@@ -301,7 +415,7 @@ struct VaryingBG {
   }
   // fields [f0, f0 + n) of one level at the corners
   template <int N>
-  __device__ __forceinline__ void blend_level(const T* L, const size_t o[4], const double w[4],
+  __device__ __forceinline__ void blend_level(const T* L, const unsigned o[4], const double w[4],
                                               int f0, double* g) const {
 #pragma unroll
     for (int q = 0; q < N; ++q)
@@ -314,7 +428,7 @@ struct VaryingBG {
       for (int i = 0; i < 11; ++i) g[i] = kNaN;
       return;
     }
-    size_t o[4];
+    unsigned o[4];
     double w[4], wt;
     cell(lon, lat, o, w);
     const T* A = level(t, wt);
@@ -331,7 +445,7 @@ struct VaryingBG {
       fu = fv = fqx = fqy = kNaN;
       return;
     }
-    size_t o[4];
+    unsigned o[4];
     double w[4], wt;
     cell(lon, lat, o, w);
     const T* A = level(t, wt);
@@ -921,8 +1035,10 @@ using KStore = KRegs<5>;
 #endif
 template <class BG>
 __global__ void __launch_bounds__(256, RWRT_WAVES_PER_SIMD) rk45_run_kernel(RunArgs<BG> a) {
-  using RayProblem = RayProblemT<BG>;
-  const RayProblem P{a.B};
+  using LBG = typename LaneBG<BG>::type;
+  using RayProblem = RayProblemT<LBG>;
+  __shared__ double cbuf[LaneBG<BG>::kLds > 0 ? LaneBG<BG>::kLds * 256 : 1];
+  const RayProblem P{LaneBG<BG>::make(a.B, cbuf + threadIdx.x)};
   const int64_t nrows = a.it_end - a.it_begin;
 #if RWRT_K_IN_LDS
   __shared__ double kbuf[5 * 5 * 256];
@@ -1059,6 +1175,8 @@ __global__ void math_kernel(int kind, int64_t n, const double* __restrict__ x,
     case 11: r = div_rearth(a); break;
     case 13: r = py_mod_2pi(a); break;
     case 14: r = py_mod_2pi_again(py_mod_2pi(a)); break;
+    case 15: r = div_hw(a, b, recip_hw(b)); break;
+    case 16: r = (double)floor_i32(a); break;
     default: r = fmod_pos(a, b); break;
   }
   out[i] = r;
@@ -1313,6 +1431,10 @@ rwrt_status make_field(const rwrt_grid* g, const double* packed, Field& F) {
   if (!(g->dlon != 0.0) || !(g->dlat != 0.0)) return fail(RWRT_ERR_ARG, "grid spacing is zero%s");
   if (reinterpret_cast<uintptr_t>(packed) % 16 != 0)
     return fail(RWRT_ERR_ARG, "packed fields must be 16-byte aligned%s");
+  // the lookups address one level with 32-bit element offsets
+  if (g->ncol > 65535 || g->nrow > 65535) return fail(RWRT_ERR_ARG, "grid dimension > 65535%s");
+  if ((int64_t)g->ncol * g->nrow >= (1LL << 24))
+    return fail(RWRT_ERR_ARG, "grid too large for one packed level (>= 2^24 records)%s");
   F.P = packed;
   F.W = g->ncol;
   F.H = g->nrow;
@@ -1754,7 +1876,7 @@ rwrt_status rwrt_kat_rk45(int32_t kind, int64_t ncol, const double* d_y0, int32_
 
 rwrt_status rwrt_selftest_math(int32_t kind, int64_t n, const double* d_x, const double* d_y,
                                double* d_out, void* stream) {
-  if (n < 0 || kind < 0 || kind > 14 || (n > 0 && (!d_x || !d_out)))
+  if (n < 0 || kind < 0 || kind > 16 || (n > 0 && (!d_x || !d_out)))
     return fail(RWRT_ERR_ARG, "bad selftest arguments%s");
   if (n == 0) return RWRT_OK;
   hipLaunchKernelGGL(math_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, kind,

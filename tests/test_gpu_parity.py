@@ -370,6 +370,25 @@ def test_device_math_exactness():
     with np.errstate(all="ignore"):
         assert np.array_equal(selftest_math("mod2pi", wrap), wrap % tp, equal_nan=True)
         assert np.array_equal(selftest_math("mod2pi_twice", wrap), (wrap % tp) % tp, equal_nan=True)
+    # shared-reciprocal division (lookup cell coordinates): bit-identical to
+    # IEEE division for every numerator/divisor, including the fallbacks
+    num = np.concatenate([wide, phys, a, [0.0, -0.0, 2.0 ** -900, -2.0 ** -901, 2.0 ** 600,
+                                          2.0 ** 599, 5e-324]])
+    for den in (0.04363323259353638, -2.5, 1.0, 3.0, 2.0 ** -100, 2.0 ** 100, 2.0 ** -101,
+                7.3e-200, 1e300, 5e-324, 0.0, -0.0, np.inf, np.nan):
+        dd = np.full(num.shape, den)
+        with np.errstate(all="ignore"):
+            assert np.array_equal(selftest_math("div_hw", num, dd), num / dd, equal_nan=True), den
+    both = rng.standard_normal(n) * 10.0 ** rng.uniform(-150, 150, n)
+    assert np.array_equal(selftest_math("div_hw", phys[:n], both), phys[:n] / both)
+    assert np.array_equal(np.signbit(selftest_math("div_hw", num, np.full(num.shape, -2.5))),
+                          np.signbit(num / -2.5))
+    # np.floor(x).astype('int32') (x86 semantics: NaN / out of range -> INT32_MIN)
+    fx = np.concatenate([a, [2.0 ** 31 - 1, 2.0 ** 31 - 0.5, 2.0 ** 31, -2.0 ** 31, -2.0 ** 31 - 1,
+                             1e300, -1e300, np.inf, -np.inf]])
+    with np.errstate(all="ignore"):
+        want = np.floor(fx).astype(np.int32).astype(np.float64)
+    assert np.array_equal(selftest_math("floor_i32", fx), want)
     rates = {}
     for name in ("sin", "cos", "tan"):
         rates[name] = float(np.mean(selftest_math(name, lat) != getattr(np, name)(lat)))
