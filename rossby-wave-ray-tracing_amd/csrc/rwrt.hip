@@ -80,27 +80,23 @@ __device__ __forceinline__ double np_min(double a, double b) {
   return (a <= b || a != a) ? a : b;
 }
 // fmod(a, b) for b > 0, exact (fmod is always exactly representable): for
-// |a| < 2^40 the integer quotient n = trunc(|a|/b) is off by at most one; the
-// remainder |a| - n b is a multiple of ulp(b) below b, so one FMA computes it
-// exactly, and a wrong n shows up as a remainder outside [0, b) (a sign test,
-// which rounding cannot flip).  A third of the library routine's cost.
-// binv (optional) ~ 1/b replaces the division: its quotient is off by at most
-// one too (relative error ~2^-52 of a quotient below 2^40), which the same
-// correction absorbs.
+// |a| < 2^40 the integer quotient n = trunc(|a|/b) is off by at most one.  The
+// remainder r = |a| - n b is a multiple of ulp(b) (or |a| itself), exact from
+// one FMA when it lies in (-b, b); a quotient one too large shows as r < 0 and
+// r + b is then the exact remainder; one too small as r >= b (possibly
+// rounded), recomputed with n + 1.  Branch-free apart from the library call
+// for huge, infinite or NaN |a|.  binv (optional) ~ 1/b replaces the
+// division: its quotient is off by at most one too (relative error ~2^-52 of
+// a quotient below 2^40), which the same correction absorbs.
 __device__ __forceinline__ double fmod_pos(double a, double b, double binv = 0.0) {
   const double x = fabs(a);
-  if (!(x < 0x1p40)) return fmod(a, b);      // NaN, inf, huge: library routine
-  double r = x;
-  if (x >= b) {
-    double n = trunc(binv != 0.0 ? x * binv : x / b);
-    r = fma(-n, b, x);
-    if (r < 0.0) {
-      n -= 1.0;
-      r = fma(-n, b, x);
-    } else if (r >= b) {
-      n += 1.0;
-      r = fma(-n, b, x);
-    }
+  const double n = trunc(binv != 0.0 ? x * binv : x / b);
+  double r = fma(-n, b, x);
+  const double lo = r + b, hi = fma(-(n + 1.0), b, x);
+  r = (r < 0.0) ? lo : ((r >= b) ? hi : r);
+  if (!(x < 0x1p40)) {
+    asm volatile("");   // NaN, inf, huge: library routine (rare branch)
+    r = fabs(fmod(a, b));
   }
   return copysign(r, a);
 }
@@ -325,12 +321,10 @@ struct CachedStaticBG {
   mutable unsigned key_x, key_y;  // cell held in the slice (~0u: none)
 
   __device__ __forceinline__ double& at(int j, int q) const { return c[(j * 11 + q) * 256]; }
+  // Only the RHS calls this: a lane with |lat| > pi/2 is masked there (its l
+  // is NaN, so are its derivatives), a NaN lat gives NaN weights; the clipped
+  // cell keeps every read in bounds either way.
   __device__ __forceinline__ void interp11(double lon, double lat, double, double g[11]) const {
-    if (!(fabs(lat) <= kHalfPi)) {
-#pragma unroll
-      for (int i = 0; i < 11; ++i) g[i] = kNaN;
-      return;
-    }
     const Corners k = corners(F, py_mod_2pi(lon), lat);
     if (k.key_x != key_x || k.key_y != key_y) {   // miss: gather the cell once
       const double* src[4] = {k.a, k.b, k.c, k.d};
@@ -477,7 +471,8 @@ __device__ __forceinline__ Merc merc_factors(double lat, double c, double s) {
 
 // The 12 Mercator outputs the hot path uses (bs.py:862-883), in the order of
 // the returned stack: fmu fmv fmux fmuy fmvx fmvy fmqx fmqy fmqxx fmqxy fmqyx fmqyy.
-__device__ __forceinline__ void mercator12(const double g[11], const Merc& M, double t, double o[12]) {
+__device__ __forceinline__ void mercator12_masked(const double g[11], const Merc& M, double t,
+                                                  double o[12]) {
   const double m = M.m, cp = M.cp;
   const double fu = g[F_U], fv = g[F_V];
   o[0] = (fu / cp) * m;                                      // fmu
@@ -492,6 +487,29 @@ __device__ __forceinline__ void mercator12(const double g[11], const Merc& M, do
   o[10] = (g[F_QXY] * cp) * m;                               // fmqyx
   o[9] = o[10] * m;                                          // fmqxy = fmqyx * mask
   o[11] = (((g[F_QYY] * cp) - (g[F_QY] * M.s)) * cp) * m;    // fmqyy
+}
+// Away from the pole mask (m == 1, cp == c: x * 1.0 and c * 1.0 + 0.0 * 1e-6
+// are the identity, NaN included) the multiplications by the mask drop out;
+// the rare masked lanes (|cos(lat)| <= 0.0175) redo the full expressions.
+__device__ __forceinline__ void mercator12(const double g[11], const Merc& M, double t, double o[12]) {
+  const double cp = M.c;
+  const double fu = g[F_U], fv = g[F_V];
+  o[0] = fu / cp;
+  o[1] = fv / cp;
+  o[2] = g[F_UX] / cp;
+  o[3] = g[F_UY] + t * fu;
+  o[4] = g[F_VX] / cp;
+  o[5] = g[F_VY] + t * fv;
+  o[6] = g[F_QX];
+  o[7] = g[F_QY] * cp;
+  o[8] = g[F_QXX];
+  o[10] = g[F_QXY] * cp;
+  o[9] = o[10];
+  o[11] = ((g[F_QYY] * cp) - (g[F_QY] * M.s)) * cp;
+  if (M.m != 1.0) {
+    asm volatile("");   // keep the masked recomputation on its (rarely taken) branch
+    mercator12_masked(g, M, t, o);
+  }
 }
 
 // cal_ugvg(mode='extent') -> core_cal_ugvg_extent (wn.py:266-294)
@@ -516,14 +534,12 @@ __device__ __forceinline__ void ugvg(double fu, double fv, double fqx, double fq
 template <class BG>
 __device__ __forceinline__ void ray_rhs(const BG& B, double t, const double* y, double* dy,
                                         double* aux = nullptr) {
-  const double lon = y[0], lat = y[1], kx = y[2], ky = y[3], amp = y[4];
-  // wr.py:508-514 -- a masked ray returns NaN for every derivative (wr.py:552-553)
-  if (fabs(lat) >= kHalfPi || fabs(ky) >= 100.0) {
-#pragma unroll
-    for (int v = 0; v < 5; ++v) dy[v] = kNaN;
-    if (aux) aux[0] = aux[1] = aux[2] = kNaN;
-    return;
-  }
+  const double lon = y[0], lat = y[1], kx = y[2];
+  // wr.py:508-514: a masked ray's l is NaN; every derivative of it is then NaN
+  // (each one depends on kap = l / k), as the reference's NaN fill
+  // (wr.py:552-553) makes them -- no branch.
+  const bool bad = fabs(lat) >= kHalfPi || fabs(y[3]) >= 100.0;
+  const double ky = bad ? kNaN : y[3], amp = y[4];
   double g[11];
   B.interp11(lon, lat, t, g);
   double s, c;
@@ -555,7 +571,7 @@ __device__ __forceinline__ void ray_rhs(const BG& B, double t, const double* y, 
   if (aux) {
     aux[0] = ug;
     aux[1] = vg;
-    aux[2] = c;
+    aux[2] = bad ? kNaN : c;
   }
 }
 
