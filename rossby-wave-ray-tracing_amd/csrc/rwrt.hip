@@ -46,6 +46,11 @@ __device__ __forceinline__ double div_rearth(double x) {
   return fma(r, kRInv, q0);
 }
 constexpr double kNaN = __builtin_nan("");
+#if RWRT_DIAG_NODIV   // timing-only diagnostic build: approximate quotients in the RHS
+#define RDIV(a, b) ((a) * __builtin_amdgcn_rcp(b))
+#else
+#define RDIV(a, b) ((a) / (b))
+#endif
 
 // rkf45.py:604-615 (Dormand-Prince 5(4)); C++ constant division is IEEE
 // correctly rounded, like Python's.
@@ -304,67 +309,115 @@ struct StaticBG {
   }
 };
 
+// Lookups in two halves, begin() and end(): the RHS issues a lookup, computes
+// what does not depend on it (sin, cos, tan of lat), then collects it.  For
+// the plain backgrounds begin() only records the point.
+struct PendingPoint {
+  double lon, lat, t;
+};
+template <class BG>
+__device__ __forceinline__ PendingPoint lookup_begin(const BG&, double lon, double lat, double t) {
+  return PendingPoint{lon, lat, t};
+}
+template <class BG>
+__device__ __forceinline__ void lookup_end(const BG& B, const PendingPoint& p, double g[11]) {
+  B.interp11(p.lon, p.lat, p.t, g);
+}
+
 // StaticBG with a per-lane cache of the last cell's four corner records (the
 // 11 hot fields of F[x0,y1], F[x1,y1], F[x0,y0], F[x1,y0]) in LDS.  The six
 // stage evaluations of an attempt lie within a fraction of a 2.5-degree cell
 // (C3: ~0.3 cell changes per 2-h interval against ~10 RHS evaluations), so a
-// lookup is usually 44 conflict-free LDS reads instead of 24 scattered 16-B
-// global gathers.  Same values, same blend: results are unchanged.
+// lookup is usually 24 conflict-free ds_read_b128 instead of 24 scattered
+// 16-B global gathers.  A lane whose cell changed refills its slice by LDS-DMA
+// (global_load_lds_dwordx4: no VGPRs, no ds_write), issued in begin() so that
+// the fill's latency overlaps the trigonometry; end() waits for it.  Same
+// values, same blend: results are unchanged.
+//
+// Slice layout (LDS-DMA writes wave base + lane * 16 B): per wave, chunk
+// (corner j, record q) of all 64 lanes at wave_base + (j * 6 + q) * 1 KiB.
 #ifndef RWRT_CELL_CACHE
 #define RWRT_CELL_CACHE 1
 #endif
-[[maybe_unused]] constexpr int kCacheVals = 44;   // 4 corners x 11 fields
+constexpr int kCacheChunks = 4 * 6;                        // 4 corners x 6 x 16 B
+constexpr int kCacheBytesPerWave = kCacheChunks * 64 * 16;  // 24 KiB
+typedef __attribute__((address_space(3))) void* lds_void_ptr;
+typedef __attribute__((address_space(1))) const void* global_void_ptr;
+
 struct CachedStaticBG {
   static constexpr bool kTimeVarying = false;
   Field F;
-  double* c;                      // this lane's slice: (corner j, field q) at c[(j * 11 + q) * 256]
+  char* wave_base;                // this wave's 24 KiB (wave-uniform)
+  unsigned lane16;                // lane * 16
   mutable unsigned key_x, key_y;  // cell held in the slice (~0u: none)
 
-  __device__ __forceinline__ double& at(int j, int q) const { return c[(j * 11 + q) * 256]; }
-  // Only the RHS calls this: a lane with |lat| > pi/2 is masked there (its l
-  // is NaN, so are its derivatives), a NaN lat gives NaN weights; the clipped
-  // cell keeps every read in bounds either way.
-  __device__ __forceinline__ void interp11(double lon, double lat, double, double g[11]) const {
+  struct Pending {
+    double wa, wb, wc, wd;
+  };
+  __device__ __forceinline__ const double2& chunk(int j, int q) const {
+    return *reinterpret_cast<const double2*>(wave_base + (j * 6 + q) * 1024 + lane16);
+  }
+  __device__ __forceinline__ Pending begin(double lon, double lat) const {
     const Corners k = corners(F, py_mod_2pi(lon), lat);
-    if (k.key_x != key_x || k.key_y != key_y) {   // miss: gather the cell once
+    if (k.key_x != key_x || k.key_y != key_y) {   // miss: refill the slice by LDS-DMA
       const double* src[4] = {k.a, k.b, k.c, k.d};
-      double2 v[4][6];   // all 24 gathers in flight before the LDS writes
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int q = 0; q < 6; ++q) v[j][q] = reinterpret_cast<const double2*>(src[j])[q];
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int q = 0; q < 11; ++q) at(j, q) = (q & 1) ? v[j][q >> 1].y : v[j][q >> 1].x;
+        for (int q = 0; q < 6; ++q)
+          __builtin_amdgcn_global_load_lds((global_void_ptr)(src[j] + 2 * q),
+                                           (lds_void_ptr)(wave_base + (j * 6 + q) * 1024), 16, 0, 0);
       key_x = k.key_x;
       key_y = k.key_y;
     }
-#pragma unroll
-    for (int q = 0; q < 11; ++q) g[q] = blend(k, at(0, q), at(1, q), at(2, q), at(3, q));
+    return Pending{k.wa, k.wb, k.wc, k.wd};
   }
+  __device__ __forceinline__ void end(const Pending& p, double g[11]) const {
+    Corners k;
+    k.wa = p.wa;
+    k.wb = p.wb;
+    k.wc = p.wc;
+    k.wd = p.wd;
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      const double2 a = chunk(0, q), b = chunk(1, q), c = chunk(2, q), d = chunk(3, q);
+      g[2 * q] = blend(k, a.x, b.x, c.x, d.x);
+      if (2 * q + 1 < 11) g[2 * q + 1] = blend(k, a.y, b.y, c.y, d.y);
+    }
+  }
+  // Only the RHS looks up through the cache: a lane with |lat| > pi/2 is
+  // masked there (its l is NaN, so are its derivatives), a NaN lat gives NaN
+  // weights; the clipped cell keeps every access in bounds either way.
   __device__ __forceinline__ void interp4(double lon, double lat, double, double& fu, double& fv,
                                           double& fqx, double& fqy) const {
     rwrt::interp4(F, py_mod_2pi(lon), lat, fu, fv, fqx, fqy);
   }
 };
+__device__ __forceinline__ CachedStaticBG::Pending lookup_begin(const CachedStaticBG& B, double lon,
+                                                                double lat, double) {
+  return B.begin(lon, lat);
+}
+__device__ __forceinline__ void lookup_end(const CachedStaticBG& B,
+                                           const CachedStaticBG::Pending& p, double g[11]) {
+  B.end(p, g);
+}
 
 // The background a persistent lane integrates with: the cached lookup for the
-// static state (kernel-owned LDS slice), the plain one otherwise.
+// static state (kernel-owned LDS), the plain one otherwise.
 template <class BG>
 struct LaneBG {
   using type = BG;
-  static constexpr int kLds = 0;
-  __device__ static BG make(const BG& B, double*) { return B; }
+  static constexpr int kLdsBytes = 0;
+  __device__ static BG make(const BG& B, char*) { return B; }
 };
 #if RWRT_CELL_CACHE
 template <>
 struct LaneBG<StaticBG> {
   using type = CachedStaticBG;
-  static constexpr int kLds = kCacheVals;
-  __device__ static CachedStaticBG make(const StaticBG& B, double* slice) {
-    return CachedStaticBG{B.F, slice, ~0u, ~0u};
+  static constexpr int kLdsBytes = 4 * kCacheBytesPerWave;   // 256-thread blocks
+  __device__ static CachedStaticBG make(const StaticBG& B, char* lds) {
+    const unsigned wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    return CachedStaticBG{B.F, lds + wave * kCacheBytesPerWave, (threadIdx.x & 63u) * 16u, ~0u, ~0u};
   }
 };
 #endif
@@ -494,11 +547,11 @@ __device__ __forceinline__ void mercator12_masked(const double g[11], const Merc
 __device__ __forceinline__ void mercator12(const double g[11], const Merc& M, double t, double o[12]) {
   const double cp = M.c;
   const double fu = g[F_U], fv = g[F_V];
-  o[0] = fu / cp;
-  o[1] = fv / cp;
-  o[2] = g[F_UX] / cp;
+  o[0] = RDIV(fu, cp);
+  o[1] = RDIV(fv, cp);
+  o[2] = RDIV(g[F_UX], cp);
   o[3] = g[F_UY] + t * fu;
-  o[4] = g[F_VX] / cp;
+  o[4] = RDIV(g[F_VX], cp);
   o[5] = g[F_VY] + t * fv;
   o[6] = g[F_QX];
   o[7] = g[F_QY] * cp;
@@ -515,13 +568,13 @@ __device__ __forceinline__ void mercator12(const double g[11], const Merc& M, do
 // cal_ugvg(mode='extent') -> core_cal_ugvg_extent (wn.py:266-294)
 __device__ __forceinline__ void ugvg(double fu, double fv, double fqx, double fqy,
                                      double k, double l, double& ug, double& vg) {
-  const double kap = l / k;
+  const double kap = RDIV(l, k);
   const double kap2 = kap * kap;
   const double kap1 = 1.0 + kap2;
   const double KK = (k * k) * kap1;
   const double denom = KK * kap1;
-  ug = fu + (((1.0 - kap2) * fqy) - ((2.0 * kap) * fqx)) / denom;
-  vg = fv + (((2.0 * kap) * fqy) + ((1.0 - kap2) * fqx)) / denom;
+  ug = fu + RDIV(((1.0 - kap2) * fqy) - ((2.0 * kap) * fqx), denom);
+  vg = fv + RDIV(((2.0 * kap) * fqy) + ((1.0 - kap2) * fqx), denom);
 }
 
 // ---------------------------------------------------------------------------
@@ -541,10 +594,25 @@ __device__ __forceinline__ void ray_rhs(const BG& B, double t, const double* y, 
   const bool bad = fabs(lat) >= kHalfPi || fabs(y[3]) >= 100.0;
   const double ky = bad ? kNaN : y[3], amp = y[4];
   double g[11];
-  B.interp11(lon, lat, t, g);
+#if !RWRT_DIAG_NOINTERP
+  const auto pending = lookup_begin(B, lon, lat, t);   // the lookup's fill overlaps the trig
+#endif
   double s, c;
+#if RWRT_DIAG_NOTRIG     // timing-only diagnostic build: polynomial stand-ins
+  s = lat * (1.0 - lat * lat * (1.0 / 6.0));
+  c = 1.0 - lat * lat * 0.5;
+  const double tn = lat * (1.0 + lat * lat * (1.0 / 3.0));
+#else
   sincos(lat, &s, &c);              // one argument reduction for both (== sin(), cos())
   const double tn = tan(lat);
+#endif
+#if RWRT_DIAG_NOINTERP   // timing-only diagnostic build: constant background
+#pragma unroll
+  for (int q = 0; q < 11; ++q) g[q] = 1e-5 * (q + 1) + 1e-9 * lat;
+#else
+  __builtin_amdgcn_sched_barrier(0);
+  lookup_end(B, pending, g);
+#endif
   const Merc M = merc_factors(lat, c, s);
   double o[12];
   mercator12(g, M, tn, o);
@@ -553,14 +621,14 @@ __device__ __forceinline__ void ray_rhs(const BG& B, double t, const double* y, 
   double ug, vg;
   ugvg(fmu, fmv, fmqx, fmqy, kx, ky, ug, vg);
   // core_diffun (wr.py:53-78); freq only feeds the dead ps/up terms
-  const double kap = ky / kx;
+  const double kap = RDIV(ky, kx);
   const double kap2 = kap * kap;
   const double kap1 = 1.0 + kap * kap;
   const double kk = (kx * kx) * kap1;
-  const double dzwn = (-kx) * ((fmux + kap * fmvx) + (kap * fmqxx - fmqyx) / kk);
-  const double dmwn = (-kx) * ((fmuy + kap * fmvy) + (kap * fmqxy - fmqyy) / kk);
-  const double damp1 = (2.0 * ((fmux + fmvy) + kap * (fmvx + fmuy))) / kap1;
-  const double damp2 = (2.0 * (kap * (fmqxx - fmqyy) + (kap2 - 1.0) * fmqxy)) / (kk * kap1);
+  const double dzwn = (-kx) * ((fmux + kap * fmvx) + RDIV(kap * fmqxx - fmqyx, kk));
+  const double dmwn = (-kx) * ((fmuy + kap * fmvy) + RDIV(kap * fmqxy - fmqyy, kk));
+  const double damp1 = RDIV(2.0 * ((fmux + fmvy) + kap * (fmvx + fmuy)), kap1);
+  const double damp2 = RDIV(2.0 * (kap * (fmqxx - fmqyy) + (kap2 - 1.0) * fmqxy), kk * kap1);
   const double damp3 = (-2.0 * s) * fmv;
   const double damp = (damp1 + damp2) + damp3;
   dy[0] = div_rearth(ug);
@@ -886,7 +954,11 @@ struct Lane {
                              P::NAUX > 0 ? aux : nullptr);
     if (en != en) en = 0.0;                 // rkf45.py:446
     if (en < 1.0) {
+#if RWRT_DIAG_NOPOW
+      double fac = np_min(kMaxFactor, kSafety / (0.5 + en));
+#else
       double fac = np_min(kMaxFactor, kSafety * pow(en, kErrExp));
+#endif
       if (en == 0.0) fac = kMaxFactor;
       if (rejected) fac = np_min(1.0, fac);
       habs = ha * fac;
@@ -900,7 +972,11 @@ struct Lane {
       ++nacc;
       return (t - tb >= 0.0) ? kReached : kStep;   // rkf45.py:250
     }
+#if RWRT_DIAG_NOPOW
+    hs = ha * np_max(kMinFactor, kSafety / (0.5 + en));
+#else
     hs = ha * np_max(kMinFactor, kSafety * pow(en, kErrExp));
+#endif
     rejected = true;
     ++nrej;
     return kStep;
@@ -1053,13 +1129,14 @@ template <class BG>
 __global__ void __launch_bounds__(256, RWRT_WAVES_PER_SIMD) rk45_run_kernel(RunArgs<BG> a) {
   using LBG = typename LaneBG<BG>::type;
   using RayProblem = RayProblemT<LBG>;
-  __shared__ double cbuf[LaneBG<BG>::kLds > 0 ? LaneBG<BG>::kLds * 256 : 1];
-  const RayProblem P{LaneBG<BG>::make(a.B, cbuf + threadIdx.x)};
+  // all LDS in one array: the stages (5 x 5 doubles per lane) then the lookup cache
+  constexpr int kKBytes = 5 * 5 * 256 * 8;
+  __shared__ __attribute__((aligned(16))) char smem[kKBytes + LaneBG<BG>::kLdsBytes];
+  const RayProblem P{LaneBG<BG>::make(a.B, smem + kKBytes)};
   const int64_t nrows = a.it_end - a.it_begin;
 #if RWRT_K_IN_LDS
-  __shared__ double kbuf[5 * 5 * 256];
   Lane<RayProblem, KStore> L;
-  L.K.p = kbuf + threadIdx.x;
+  L.K.p = reinterpret_cast<double*>(smem) + threadIdx.x;
   L.K.stride = 256;
 #else
   Lane<RayProblem, KStore> L;
@@ -1121,7 +1198,11 @@ __global__ void __launch_bounds__(256, RWRT_WAVES_PER_SIMD) rk45_run_kernel(RunA
     bool masked = fabs(y[1]) >= kHalfPi;
     if (!masked) {
       cos_c = have ? L.aux[2] : cos(y[1]);
+#if RWRT_DIAG_NOPOST
+      masked = fabs(y[1] - prev_lat) >= a.cut_off;
+#else
       masked = cal_dis_c(y[0], y[1], prev_lon, prev_lat, cos_c, cos_prev) >= a.cut_off;
+#endif
     }
     if (masked) {
 #pragma unroll
