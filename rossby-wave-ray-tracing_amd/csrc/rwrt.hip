@@ -378,12 +378,29 @@ struct CachedStaticBG {
     k.wb = p.wb;
     k.wc = p.wc;
     k.wd = p.wd;
+#ifndef RWRT_LDS_BATCH
+#define RWRT_LDS_BATCH 1
+#endif
+#if RWRT_LDS_BATCH
+    double2 v[4][6];   // every read in flight before the first blend
+#pragma unroll
+    for (int q = 0; q < 6; ++q)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j][q] = chunk(j, q);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      g[2 * q] = blend(k, v[0][q].x, v[1][q].x, v[2][q].x, v[3][q].x);
+      if (2 * q + 1 < 11) g[2 * q + 1] = blend(k, v[0][q].y, v[1][q].y, v[2][q].y, v[3][q].y);
+    }
+#else
 #pragma unroll
     for (int q = 0; q < 6; ++q) {
       const double2 a = chunk(0, q), b = chunk(1, q), c = chunk(2, q), d = chunk(3, q);
       g[2 * q] = blend(k, a.x, b.x, c.x, d.x);
       if (2 * q + 1 < 11) g[2 * q + 1] = blend(k, a.y, b.y, c.y, d.y);
     }
+#endif
   }
   // Only the RHS looks up through the cache: a lane with |lat| > pi/2 is
   // masked there (its l is NaN, so are its derivatives), a NaN lat gives NaN
@@ -669,6 +686,21 @@ __device__ __forceinline__ double cal_dis_c(double lon_c, double lat_c, double l
   const double sl = sin((lon_c - lon_p) / 2.0);
   const double a = sd * sd + (cos_p * cos_c) * (sl * sl);
   return fabs(2.0 * atan2(sqrt(a), sqrt(1.0 - a)));
+}
+// cal_dis_c(...) >= cut_off, with the atan2 skipped when the haversine
+// argument is certainly below the threshold (cut_a: haversine_cut on the host)
+__device__ __forceinline__ bool cal_dis_reaches(double lon_c, double lat_c, double lon_p,
+                                                double lat_p, double cos_c, double cos_p,
+                                                double cut_off, double cut_a) {
+  const double sd = sin((lat_c - lat_p) / 2.0);
+  const double sl = sin((lon_c - lon_p) / 2.0);
+  const double a = sd * sd + (cos_p * cos_c) * (sl * sl);
+  bool r = false;
+  if (!(a < cut_a)) {
+    asm volatile("");   // rare: near or past the threshold, or NaN
+    r = fabs(2.0 * atan2(sqrt(a), sqrt(1.0 - a))) >= cut_off;
+  }
+  return r;
 }
 
 // ---------------------------------------------------------------------------
@@ -1103,7 +1135,19 @@ struct RunArgs {
   int32_t* queue;       // [0] heavy-queue head, [1] light-queue head
   int64_t n_heavy;      // order[0, n_heavy) = heavy queue, the rest = light queue
   int32_t heavy_blocks; // blocks [0, heavy_blocks) serve the heavy queue first
+  double cut_a;         // haversine argument certainly below cut_off (cal_dis_below)
 };
+
+// Haversine threshold: d = 2 atan2(sqrt(a), sqrt(1 - a)) increases with a, so
+// a < sin^2(cut_off / 2) (1 - 1e-9) proves d < cut_off for the computed d too
+// (its error is ~1e-15 relative) -- the common "no jump" verdict of wr.py:844-850
+// without the atan2 and the two square roots.  Any other a (near or above the
+// threshold, > 1, NaN) takes the full cal_dis.  -1 disables the shortcut.
+inline double haversine_cut(double cut_off) {
+  if (!(cut_off > 0.0 && cut_off <= 3.0)) return -1.0;
+  const double s = std::sin(0.5 * cut_off);
+  return s * s * (1.0 - 1e-9);
+}
 
 // WR.core_ray_run_rk45 (wr.py:767-887) for rows [it_begin, it_end): persistent
 // lanes, one ray each, refilled from the work queue.
@@ -1201,7 +1245,7 @@ __global__ void __launch_bounds__(256, RWRT_WAVES_PER_SIMD) rk45_run_kernel(RunA
 #if RWRT_DIAG_NOPOST
       masked = fabs(y[1] - prev_lat) >= a.cut_off;
 #else
-      masked = cal_dis_c(y[0], y[1], prev_lon, prev_lat, cos_c, cos_prev) >= a.cut_off;
+      masked = cal_dis_reaches(y[0], y[1], prev_lon, prev_lat, cos_c, cos_prev, a.cut_off, a.cut_a);
 #endif
     }
     if (masked) {
@@ -1618,7 +1662,7 @@ rwrt_status launch_run(const BG& B, int64_t nray, const rwrt_params* p, const do
   const int heavy_blocks = (d_order && n_heavy > 0 && blocks >= 2 * (int64_t)ncu) ? ncu : 0;
   RunArgs<BG> a{B, nray, p->rtol, p->atol, p->min_step, p->cut_off, p->nt, it_begin, it_end,
                 d_tbound, d_order, d_state, d_count, d_nanrow, d_out, d_work,
-                heavy_blocks ? n_heavy : 0, heavy_blocks};
+                heavy_blocks ? n_heavy : 0, heavy_blocks, haversine_cut(p->cut_off)};
   hipLaunchKernelGGL(rk45_run_kernel<BG>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
   return check_launch("rk45_run_kernel");
 }
