@@ -383,6 +383,14 @@ def test_device_math_exactness():
     assert np.array_equal(selftest_math("div_hw", phys[:n], both), phys[:n] / both)
     assert np.array_equal(np.signbit(selftest_math("div_hw", num, np.full(num.shape, -2.5))),
                           np.signbit(num / -2.5))
+    # the RHS's fused sin/cos/tan (one reduction, ocml's algorithms restated) is
+    # bit-identical to the library sin(), cos(), tan()
+    tr = np.concatenate([lat, rng.uniform(-4, 4, n), rng.uniform(-1e6, 1e6, 1000) * 10.0 ** rng.uniform(-300, 3, 1000),
+                         np.pi / 4 * np.arange(-40, 41), np.nextafter(np.pi / 4 * np.arange(-40, 41), 9),
+                         [0.0, -0.0, 5e-324, -1e-310, 2.0 ** 30, -2.0 ** 30 + 1, 1e300, np.inf, -np.inf, np.nan]])
+    for name in ("sin", "cos", "tan"):
+        assert np.array_equal(selftest_math("sct_" + name, tr).view(np.int64),
+                              selftest_math(name, tr).view(np.int64)), name
     # np.floor(x).astype('int32') (x86 semantics: NaN / out of range -> INT32_MIN)
     fx = np.concatenate([a, [2.0 ** 31 - 1, 2.0 ** 31 - 0.5, 2.0 ** 31, -2.0 ** 31, -2.0 ** 31 - 1,
                              1e300, -1e300, np.inf, -np.inf]])
