@@ -93,8 +93,10 @@ def find_traffic(path, workload, schedule):
     """Per-launch HBM bytes of the ray kernel from a PMC profile of this workload
     run with the same launch schedule (rows per launch)."""
     import glob
+    # newest profile first by path (profiles/<round>/<version>/...: sorts the
+    # same in any checkout, unlike file times)
     cands = [path] if path else sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "traffic.json"), recursive=True),
-                                       key=os.path.getmtime, reverse=True)
+                                       reverse=True)
     for c in cands:
         try:
             t = json.load(open(c))

@@ -946,9 +946,9 @@ __device__ __forceinline__ double stage_input(const KS& K, double t, const doubl
 }
 
 // One DP5(4) attempt: rk_step (rkf45.py:259-321) + _estimate_error_norm
-// (rkf45.py:368-373).  The six stage evaluations share ONE inlined copy of the
-// RHS (a wave-uniform stage loop), which keeps the kernel's code small and its
-// register file for occupancy.  Returns the error norm (NaN kept); fills y_new,
+// (rkf45.py:368-373).  The six stage evaluations are unrolled (six inlined RHS
+// copies, ~45 KB of code: fits the instruction cache; RWRT_UNROLL_STAGES=0
+// keeps one copy in a wave-uniform stage loop).  Returns the error norm (NaN kept); fills y_new,
 // K6, if aux is given the problem's side outputs of the K6 evaluation (at
 // y_new), and if Kout is given all seven stages.
 template <class P, class KS>
@@ -959,7 +959,14 @@ __device__ __forceinline__ double dp54_attempt(const P& fun, KS& K, double t, co
                                                double* aux = nullptr) {
   constexpr int NV = P::NV;
   double ys[NV], r[NV];
+#ifndef RWRT_UNROLL_STAGES
+#define RWRT_UNROLL_STAGES 1   // six inlined RHS copies: no stage dispatch (the code fits the I-cache)
+#endif
+#if RWRT_UNROLL_STAGES
+#pragma unroll
+#else
 #pragma nounroll
+#endif
   for (int s = 1; s <= 6; ++s) {
     double ts;
     switch (s) {   // wave-uniform: one straight-line combination per stage
