@@ -38,12 +38,19 @@ constexpr double kRInv = 1.0 / 6.3712e6;   // RN(1 / R)
 // FMA rounds q0 + r/R correctly.  Zero, tiny, huge and non-finite x take the
 // IEEE division (signed zeros, gradual underflow).  Verified bit-exact against
 // IEEE division on the device (tests/test_gpu_parity.py).
+// A zero x stays on the fast path (q0 = x * RN(1/R) is the correctly signed
+// zero, kept by the copysign): in a zonal flow dk/dt is exactly -0 for every
+// ray, so the fallback would otherwise run on every evaluation.
 __device__ __forceinline__ double div_rearth(double x) {
   const double ax = fabs(x);
-  if (!(ax > 0x1p-900 && ax < 0x1p900)) return x / kREarth;
   const double q0 = x * kRInv;
   const double r = fma(-q0, kREarth, x);
-  return fma(r, kRInv, q0);
+  double q = copysign(fma(r, kRInv, q0), q0);
+  if (!(ax < 0x1p900) | ((ax < 0x1p-900) & (ax != 0.0))) {
+    asm volatile("");   // tiny, huge, infinite or NaN: IEEE division (rare branch)
+    q = x / kREarth;
+  }
+  return q;
 }
 constexpr double kNaN = __builtin_nan("");
 #if RWRT_DIAG_NODIV   // timing-only diagnostic build: approximate quotients in the RHS

@@ -355,6 +355,10 @@ def test_device_math_exactness():
         assert np.array_equal(selftest_math("div_rearth", wide), wide / 6.3712e6, equal_nan=True)
     phys = rng.standard_normal(4 * n) * 10.0 ** rng.uniform(-12, 4, 4 * n)
     assert np.array_equal(selftest_math("div_rearth", phys), phys / 6.3712e6)
+    zeros = np.array([0.0, -0.0, 1e-300, -1e-300, 2.0 ** -900, -(2.0 ** -900), 2.0 ** 900])
+    with np.errstate(all="ignore"):
+        dz = selftest_math("div_rearth", zeros)
+        assert np.array_equal(dz.view(np.int64), (zeros / 6.3712e6).view(np.int64))
     tp = 2 * np.pi
     near = np.concatenate([np.arange(-200, 200) * tp, np.nextafter(np.arange(-200, 200) * tp, np.inf),
                            np.nextafter(np.arange(-200, 200) * tp, -np.inf),
