@@ -426,25 +426,7 @@ __device__ __forceinline__ void lookup_end(const CachedStaticBG& B,
   B.end(p, g);
 }
 
-// The background a persistent lane integrates with: the cached lookup for the
-// static state (kernel-owned LDS), the plain one otherwise.
-template <class BG>
-struct LaneBG {
-  using type = BG;
-  static constexpr int kLdsBytes = 0;
-  __device__ static BG make(const BG& B, char*) { return B; }
-};
-#if RWRT_CELL_CACHE
-template <>
-struct LaneBG<StaticBG> {
-  using type = CachedStaticBG;
-  static constexpr int kLdsBytes = 4 * kCacheBytesPerWave;   // 256-thread blocks
-  __device__ static CachedStaticBG make(const StaticBG& B, char* lds) {
-    const unsigned wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    return CachedStaticBG{B.F, lds + wave * kCacheBytesPerWave, (threadIdx.x & 63u) * 16u, ~0u, ~0u};
-  }
-};
-#endif
+
 
 template <class T>
 struct VaryingBG {
@@ -456,6 +438,11 @@ struct VaryingBG {
 
   // cell corners and weights: the arithmetic of corners() (interpolation.py:77-135)
   __device__ __forceinline__ void cell(double lon, double lat, unsigned o[4], double w[4]) const {
+    unsigned kx, ky;
+    cell(lon, lat, o, w, kx, ky);
+  }
+  __device__ __forceinline__ void cell(double lon, double lat, unsigned o[4], double w[4],
+                                       unsigned& key_x, unsigned& key_y) const {
     const double lons = py_mod_2pi_again(py_mod_2pi(lon));
     const double x = div_uniform(lons - lon0, dlon);
     const double y = div_uniform(lat - lat0, dlat);
@@ -472,12 +459,19 @@ struct VaryingBG {
     w[1] = sx * sy;
     w[2] = (1.0 - sx) * (1.0 - sy);
     w[3] = sx * (1.0 - sy);
+    key_x = (unsigned)x0 | ((unsigned)x1 << 16);
+    key_y = (unsigned)y0 | ((unsigned)y1 << 16);
   }
   // level index and weight of time t
   __device__ __forceinline__ const T* level(double t, double& wt) const {
+    int j;
+    return level(t, wt, j);
+  }
+  __device__ __forceinline__ const T* level(double t, double& wt, int& jlev) const {
     const double s = (t - t0) / dt;
     const int64_t j = (nlev > 1) ? (int64_t)clip(floor_i32(s), nlev - 2) : 0;
     wt = np_min(np_max(s - (double)j, 0.0), 1.0);
+    jlev = (int)j;
     return P + j * lev_stride;
   }
   __device__ __forceinline__ static double bl(const double w[4], double a, double b, double c,
@@ -532,6 +526,115 @@ struct VaryingBG {
     fqy = c[1] * (1.0 - wt) + d[1] * wt;
   }
 };
+
+// VaryingBG<float> with the same per-lane LDS cache, keyed by (cell, level
+// pair): both bracketing levels' four fp32 corner records (2 x 4 x 48 B = 24
+// chunks of 16 B, the same 24 KiB per wave as the static cache).  A lane
+// refills when its cell or its level pair changes (every dt of ray time).
+// fp64 levels would need twice the LDS and stay on plain gathers.
+struct CachedVaryingBG32 {
+  static constexpr bool kTimeVarying = true;
+  VaryingBG<float> V;
+  char* wave_base;
+  unsigned lane16;
+  mutable unsigned key_x, key_y;
+  mutable int key_j;
+
+  struct Pending {
+    double w[4];
+    double wt;
+  };
+  __device__ __forceinline__ float4 chunk(int lev, int j, int q) const {
+    return *reinterpret_cast<const float4*>(wave_base + ((lev * 4 + j) * 3 + q) * 1024 + lane16);
+  }
+  __device__ __forceinline__ Pending begin(double lon, double lat, double t) const {
+    Pending p;
+    unsigned o[4], kx, ky;
+    int jl;
+    V.cell(lon, lat, o, p.w, kx, ky);
+    const float* A = V.level(t, p.wt, jl);
+    if (kx != key_x || ky != key_y || jl != key_j) {   // miss: refill by LDS-DMA
+      const float* L[2] = {A, A + (V.nlev > 1 ? V.lev_stride : 0)};
+#pragma unroll
+      for (int lev = 0; lev < 2; ++lev)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int q = 0; q < 3; ++q)
+            __builtin_amdgcn_global_load_lds((global_void_ptr)(L[lev] + o[j] + 4 * q),
+                                             (lds_void_ptr)(wave_base + ((lev * 4 + j) * 3 + q) * 1024),
+                                             16, 0, 0);
+      key_x = kx;
+      key_y = ky;
+      key_j = jl;
+    }
+    return p;
+  }
+  __device__ __forceinline__ void end(const Pending& p, double g[11]) const {
+    float4 v[2][4][3];
+#pragma unroll
+    for (int lev = 0; lev < 2; ++lev)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) v[lev][j][q] = chunk(lev, j, q);
+    __builtin_amdgcn_sched_barrier(0);
+    double ga[11], gb[11];
+#pragma unroll
+    for (int f = 0; f < 11; ++f) {
+      const int q = f >> 2, e = f & 3;
+      auto el = [&](int lev, int j) -> double {
+        const float4& c = v[lev][j][q];
+        return (double)(e == 0 ? c.x : e == 1 ? c.y : e == 2 ? c.z : c.w);
+      };
+      ga[f] = VaryingBG<float>::bl(p.w, el(0, 0), el(0, 1), el(0, 2), el(0, 3));
+      gb[f] = VaryingBG<float>::bl(p.w, el(1, 0), el(1, 1), el(1, 2), el(1, 3));
+    }
+#pragma unroll
+    for (int i = 0; i < 11; ++i) g[i] = ga[i] * (1.0 - p.wt) + gb[i] * p.wt;
+  }
+  __device__ __forceinline__ void interp4(double lon, double lat, double t, double& fu, double& fv,
+                                          double& fqx, double& fqy) const {
+    V.interp4(lon, lat, t, fu, fv, fqx, fqy);
+  }
+};
+__device__ __forceinline__ CachedVaryingBG32::Pending lookup_begin(const CachedVaryingBG32& B, double lon,
+                                                                   double lat, double t) {
+  return B.begin(lon, lat, t);
+}
+__device__ __forceinline__ void lookup_end(const CachedVaryingBG32& B,
+                                           const CachedVaryingBG32::Pending& p, double g[11]) {
+  B.end(p, g);
+}
+
+// The background a persistent lane integrates with: the cached lookup for the
+// static state (kernel-owned LDS), the plain one otherwise.
+template <class BG>
+struct LaneBG {
+  using type = BG;
+  static constexpr int kLdsBytes = 0;
+  __device__ static BG make(const BG& B, char*) { return B; }
+};
+#if RWRT_CELL_CACHE
+template <>
+struct LaneBG<StaticBG> {
+  using type = CachedStaticBG;
+  static constexpr int kLdsBytes = 4 * kCacheBytesPerWave;   // 256-thread blocks
+  __device__ static CachedStaticBG make(const StaticBG& B, char* lds) {
+    const unsigned wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    return CachedStaticBG{B.F, lds + wave * kCacheBytesPerWave, (threadIdx.x & 63u) * 16u, ~0u, ~0u};
+  }
+};
+template <>
+struct LaneBG<VaryingBG<float>> {
+  using type = CachedVaryingBG32;
+  static constexpr int kLdsBytes = 4 * kCacheBytesPerWave;
+  __device__ static CachedVaryingBG32 make(const VaryingBG<float>& B, char* lds) {
+    const unsigned wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    return CachedVaryingBG32{B, lds + wave * kCacheBytesPerWave, (threadIdx.x & 63u) * 16u, ~0u, ~0u, -1};
+  }
+};
+#endif
 
 // ---------------------------------------------------------------------------
 // sin, cos and tan of one argument with ONE reduction: the ROCm device
