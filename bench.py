@@ -89,6 +89,26 @@ def cpu_baseline(bg, y0, nrays, days, seed=0):
     return pick, hist, int(nacc.sum()), dt, nt
 
 
+def devmath_check(bg, y0, pick, gpu, nt, nrays=2048):
+    """Bit-identity of the GPU rows with the oracle run on the device's own
+    sin/cos/tan/pow (rwrt_oracle.device_math(), tests/test_gpu_devmath.py):
+    the first ``nrays`` rays of the CPU sample, every row, all 7 variables."""
+    import rwrt_oracle as O
+    try:
+        O._devmath_lib()
+    except (RuntimeError, OSError) as e:
+        return {"skipped": str(e)}
+    sel = pick[:nrays]
+    with np.errstate(all="ignore"), O.device_math():
+        hist, _, _, _ = O.ray_run(O.Background(**bg), y0[:, sel].copy(), nt, 7200.0)
+    g = np.transpose(gpu[:len(sel)], (2, 1, 0))            # (7, rows 1.., ray)
+    c = hist[:, 1:]
+    same = (g == c) | (np.isnan(g) & np.isnan(c))
+    return {"rays": int(len(sel)), "rows": int(nt - 1), "horizon_days": (nt - 1) / 12.0,
+            "identical_values_frac": float(same.mean()),
+            "rays_identical_all_rows": int(same.all(axis=(0, 1)).sum())}
+
+
 def find_traffic(path, workload, schedule):
     """Per-launch HBM bytes of the ray kernel from a PMC profile of this workload
     run with the same launch schedule (rows per launch)."""
@@ -270,11 +290,11 @@ def main():
             # parity of the same sample on the GPU after the same horizon
             rows = {}
             eng.integrate(torch.as_tensor(y0[:, pick], device=dev), cnt, 7200.0,
-                          sink=lambda a, b, o: rows.__setitem__(a, o[:, :, :2].cpu().numpy()))
+                          sink=lambda a, b, o: rows.__setitem__(a, o[:, :, :7].cpu().numpy()))
             gpu = np.concatenate([rows[k] for k in sorted(rows)], axis=1)   # rows 1..cnt-1
             parity = []
             for row in sorted({min(12, cnt - 1), cnt - 1}):
-                g, c = gpu[:, row - 1], hist[:2, row].T
+                g, c = gpu[:, row - 1, :2], hist[:2, row].T
                 ok = ~np.isnan(g).any(1) & ~np.isnan(c).any(1)
                 d = np.max(np.abs(g[ok] - c[ok]), axis=1) if ok.any() else np.zeros(1)
                 parity.append({"horizon_days": row / 12.0, "rays": int(ok.sum()),
@@ -282,6 +302,7 @@ def main():
                                "max": float(d.max()),
                                "alive_mismatch": int(np.sum(np.isnan(g[:, 0]) != np.isnan(c[:, 0])))})
             result["max_dpos_vs_cpu_rad"] = parity
+            result["bitwise_vs_cpu_devmath"] = devmath_check(bg, y0, pick, gpu, cnt)
         print(json.dumps(result))
     if dist:
         dist.barrier()

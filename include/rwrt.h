@@ -226,7 +226,11 @@ rwrt_status rwrt_kat_rk45(int32_t kind, int64_t ncol, const double* d_y0,
  * 4 atan2(x, y), 5 Python x % y (fmod-based), 6 sqrt(x), 7 x / y, 8 floor(x),
  * 9/10 sin/cos through sincos(x), 11 x / 6.3712e6 (the kernels' exact division
  * by the earth radius), 12 fmod(x, y) for y > 0 (the kernels' exact fmod),
- * 13 x % (2 pi) and 14 (x % (2 pi)) % (2 pi) as the kernels evaluate them.
+ * 13 x % (2 pi) and 14 (x % (2 pi)) % (2 pi) as the kernels evaluate them,
+ * 15 x / y by a shared reciprocal, 16 np.floor(x).astype(int32),
+ * 17/18/19 sin/cos/tan from the fused one-reduction routine, 20 pow(x, y) and
+ * 21 exp(x) as restated in csrc/rwrt_math.h, 22 the refined reciprocal
+ * (v_rcp_f64 + two Newton steps) of x.
  * Lets the tests prove which operations are bit-exact on the GPU (IEEE
  * division, sqrt, fmod) and measure the last-bit agreement of the rest. */
 rwrt_status rwrt_selftest_math(int32_t kind, int64_t n, const double* d_x,

@@ -57,6 +57,74 @@ ERR_EXP = -1 / (4 + 1)        # rkf45.py:360, error_estimator_order = 4
 
 
 # ----------------------------------------------------------------------------
+# transcendentals of the ray loop: NumPy's (glibc sin/cos, SVML tan/power on
+# AVX-512 hosts -- what the reference computes with) by default;
+# ``device_math()`` swaps in the GPU's own (oracle/devmath.cpp, the kernel's
+# rwrt_math.h compiled for the host) so that the oracle and the GPU differ in
+# nothing and whole trajectories compare bit for bit.
+# ----------------------------------------------------------------------------
+class _LibM:
+    sin = staticmethod(np.sin)
+    cos = staticmethod(np.cos)
+    tan = staticmethod(np.tan)
+    power = staticmethod(np.power)
+
+
+LIBM = _LibM()
+_DEVMATH = None
+
+
+def _devmath_lib():
+    global _DEVMATH
+    if _DEVMATH is None:
+        import ctypes
+        import os
+        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_devmath", "libdevmath.so")
+        if not os.path.exists(path):
+            raise RuntimeError(f"{path} missing: build it with `make -C oracle`")
+        lib = ctypes.CDLL(path)
+        P, I = ctypes.c_void_p, ctypes.c_int64
+        for name in ("dm_sin", "dm_cos", "dm_tan", "dm_exp"):
+            getattr(lib, name).argtypes = [P, P, I]
+        lib.dm_pow.argtypes = [P, P, I, P, I]
+        _DEVMATH = lib
+    return _DEVMATH
+
+
+def _dm_unary(name):
+    def f(x):
+        x = np.asarray(x, np.float64)
+        xc = np.ascontiguousarray(x)
+        out = np.empty_like(xc)
+        getattr(_devmath_lib(), name)(xc.ctypes.data, out.ctypes.data, xc.size)
+        return out.reshape(x.shape)
+    return f
+
+
+def _dm_power(x, y):
+    x, y = np.broadcast_arrays(np.asarray(x, np.float64), np.asarray(y, np.float64))
+    xc, yc = np.ascontiguousarray(x), np.ascontiguousarray(y)
+    out = np.empty(xc.shape)
+    _devmath_lib().dm_pow(xc.ctypes.data, yc.ctypes.data, 1, out.ctypes.data, xc.size)
+    return out
+
+
+class device_math:
+    """Context manager: the oracle uses the GPU's sin/cos/tan/power inside."""
+
+    def __enter__(self):
+        _devmath_lib()
+        self._saved = (LIBM.sin, LIBM.cos, LIBM.tan, LIBM.power)
+        LIBM.sin, LIBM.cos, LIBM.tan = _dm_unary("dm_sin"), _dm_unary("dm_cos"), _dm_unary("dm_tan")
+        LIBM.power = _dm_power
+        return LIBM
+
+    def __exit__(self, *exc):
+        LIBM.sin, LIBM.cos, LIBM.tan, LIBM.power = self._saved
+        return False
+
+
+# ----------------------------------------------------------------------------
 # basic state  (bs.py)
 # ----------------------------------------------------------------------------
 class Background:
@@ -233,7 +301,7 @@ def mercator_point(bg, lon, lat, t=None):
         vals[:, ok] = _bilinear(bg.fields, c).T
     (fu, fv, fux, fuy, fvx, fvy, fqx, fqy, fqxx, fqxy, fqyx, fqyy,
      fqxxx, fqxxy, fqxyy, fqyyy, fqyxx, fqyyx) = vals
-    c, s, t = np.cos(lat), np.sin(lat), np.tan(lat)
+    c, s, t = LIBM.cos(lat), LIBM.sin(lat), LIBM.tan(lat)
     m = np.ones(c.shape)
     m[np.abs(c) <= 0.0175] = 0
     c = c * m + (1 - m) * 1e-6
@@ -276,8 +344,8 @@ def rhs(bg, y, t=None):
     dl = -kx * ((fmuy + kap * fmvy) + (kap * fmqxy - fmqyy) / kk)
     damp = (2.0 * (fmux + fmvy + kap * (fmvx + fmuy)) / kap1
             + 2.0 * (kap * (fmqxx - fmqyy) + (kap2 - 1.0) * fmqxy) / (kk * kap1)
-            + -2.0 * np.sin(lat) * fmv)
-    d = np.array([ug / R_EARTH, vg * np.cos(lat) / R_EARTH, dk / R_EARTH,
+            + -2.0 * LIBM.sin(lat) * fmv)
+    d = np.array([ug / R_EARTH, vg * LIBM.cos(lat) / R_EARTH, dk / R_EARTH,
                   dl / R_EARTH, damp * amp / R_EARTH])
     d[:, bad] = np.nan
     return d, bad
@@ -304,7 +372,7 @@ def initial_step(fun, t0, y0, f0, rtol, atol):
         import warnings
         with warnings.catch_warnings():
             warnings.simplefilter("ignore")
-            h1 = (0.01 / np.nanmax([d1, d2], axis=0)) ** (1 / 5)
+            h1 = LIBM.power(0.01 / np.nanmax([d1, d2], axis=0), 1 / 5)
     tiny = ~(d1 > 1e-15) & ~(d2 > 1e-15)
     h1[tiny] = np.maximum(1e-6, h0 * 1e-3)[tiny]
     return np.minimum(100 * h0, h1)
@@ -412,10 +480,10 @@ class DP54:
             en = error_norm(K, h, y[:, idx], yn, self.rtol, self.atol)
             ok = en < 1
             with np.errstate(divide="ignore"):
-                grow = np.minimum(MAX_FACTOR, SAFETY * en ** ERR_EXP)
+                grow = np.minimum(MAX_FACTOR, SAFETY * LIBM.power(en, ERR_EXP))
                 grow[en == 0] = MAX_FACTOR
                 grow = np.where(rejected[idx], np.minimum(1.0, grow), grow)
-                shrink = np.maximum(MIN_FACTOR, SAFETY * en ** ERR_EXP)
+                shrink = np.maximum(MIN_FACTOR, SAFETY * LIBM.power(en, ERR_EXP))
             ha = np.where(ok, ha * grow, ha * shrink)
             hs[idx] = ha
             acc_i, rej_i = idx[ok], idx[~ok]
@@ -435,8 +503,8 @@ class DP54:
 # ----------------------------------------------------------------------------
 def cal_dis(lon_c, lat_c, lon_p, lat_p):
     """wr.py:97-112 (haversine)."""
-    a = np.sin((lat_c - lat_p) / 2.0) ** 2 \
-        + np.cos(lat_p) * np.cos(lat_c) * np.sin((lon_c - lon_p) / 2.0) ** 2
+    a = LIBM.sin((lat_c - lat_p) / 2.0) ** 2 \
+        + LIBM.cos(lat_p) * LIBM.cos(lat_c) * LIBM.sin((lon_c - lon_p) / 2.0) ** 2
     return np.abs(2 * np.arctan2(np.sqrt(a), np.sqrt(1.0 - a)))
 
 

@@ -638,105 +638,39 @@ struct LaneBG<VaryingBG<float>> {
 
 // ---------------------------------------------------------------------------
 // sin, cos and tan of one argument with ONE reduction: the ROCm device
-// library's (ocml) f64 algorithms restated operation for operation --
-// __ocmlpriv_trigredsmall_f64 (Cody-Waite, 3-part pi/2), __ocmlpriv_
-// sincosred2_f64 and __ocmlpriv_tanred2_f64 with their coefficients, and the
-// sign/quadrant logic of __ocml_sincos_f64 / __ocml_tan_f64 -- so every bit
-// equals sin(), cos() and tan() (tests/test_gpu_parity.py::
-// test_device_math_exactness).  The Horner steps are written as explicit
-// three-operand v_fma_f64 (the compiler's fmac form copies each hoisted
-// coefficient first: one extra instruction per step).  |x| >= 2^30, inf and
-// NaN take the library routines.
+// library's (ocml) f64 algorithms restated operation for operation in
+// rwrt_math.h, so every bit equals sin(), cos() and tan()
+// (tests/test_gpu_parity.py::test_device_math_exactness).  The Horner steps
+// are explicit three-operand v_fma_f64 (the compiler's fmac form copies each
+// hoisted coefficient first: one extra instruction per step).  |x| >= 2^30,
+// inf and NaN take the library routines.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ double fma3(double a, double b, double c) {
   double d;
   asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
   return d;
 }
-__device__ __forceinline__ double bits_f64(unsigned long long u) { return __longlong_as_double((long long)u); }
+// ocml's refined reciprocal (v_rcp_f64 + two Newton steps)
+__device__ __forceinline__ double recip2(double b) {
+  double rc = __builtin_amdgcn_rcp(b);
+  rc = fma(fma(-b, rc, 1.0), rc, rc);
+  return fma(fma(-b, rc, 1.0), rc, rc);
+}
+}  // namespace rwrt
+#define RM_FN __device__ __forceinline__
+#define RM_FMA3(a, b, c) ::rwrt::fma3(a, b, c)
+#define RM_RECIP2(b) ::rwrt::recip2(b)
+#include "rwrt_math.h"
+namespace rwrt {
+using rwrt_math::rm_pow;
 __device__ __forceinline__ void sincostan(double x, double& sn, double& cs, double& tn) {
-  const double ax = fabs(x);
-  if (!(ax < 0x1p30)) {
+  if (!(fabs(x) < 0x1p30)) {
     asm volatile("");   // large, infinite or NaN argument: library routines (rare branch)
     sincos(x, &sn, &cs);
     tn = tan(x);
     return;
   }
-  // __ocmlpriv_trigredsmall_f64
-  const double n = rint(ax * bits_f64(0x3FE45F306DC9C883ull));
-  const double a = fma(n, bits_f64(0xBFF921FB54442D18ull), ax);
-  const double b = fma(n, bits_f64(0xBC91A62633145C00ull), a);
-  const double p = n * bits_f64(0x3C91A62633145C00ull);
-  const double pl = fma(n, bits_f64(0x3C91A62633145C00ull), -p);
-  const double s1 = a - p;
-  const double s2 = (a - s1) - p;
-  const double e = (((s1 - b) + s2) - pl);
-  const double e2 = fma(n, bits_f64(0xB97B839A252049C0ull), e);
-  const double rh = b + e2;                 // reduced argument, head
-  const double rl = e2 - (rh - b);          // and tail
-  const int q = (int)n & 3;
-  // __ocmlpriv_sincosred2_f64(rh, rl)
-  const double x2 = rh * rh;
-  const double r = x2 * 0.5;
-  const double t = 1.0 - r;
-  const double u = (1.0 - t) - r;
-  const double x4 = x2 * x2;
-  double c = fma3(x2, bits_f64(0xBDA907DB46CC5E42ull), bits_f64(0x3E21EEB69037AB78ull));
-  c = fma3(x2, c, bits_f64(0xBE927E4FA17F65F6ull));
-  c = fma3(x2, c, bits_f64(0x3EFA01A019F4EC90ull));
-  c = fma3(x2, c, bits_f64(0xBF56C16C16C16967ull));
-  c = fma3(x2, c, bits_f64(0x3FA5555555555555ull));
-  const double cosr = t + fma(x4, c, fma(rh, -rl, u));
-  double sp = fma3(x2, bits_f64(0x3DE5E0B2F9A43BB8ull), bits_f64(0xBE5AE600B42FDFA7ull));
-  sp = fma3(x2, sp, bits_f64(0x3EC71DE3796CDE01ull));
-  sp = fma3(x2, sp, bits_f64(0xBF2A01A019E83E5Cull));
-  sp = fma3(x2, sp, bits_f64(0x3F81111111110BB3ull));
-  const double m = rh * (-x2);
-  const double sq = fma(x2, fma(m, sp, rl * 0.5), -rl);
-  const double sinr = rh - fma(m, bits_f64(0xBFC5555555555555ull), sq);
-  // __ocml_sincos_f64 quadrant and sign
-  const unsigned long long sgn_hi = (q > 1) ? 0x8000000000000000ull : 0ull;
-  const unsigned long long xsgn = (unsigned long long)__double_as_longlong(x) & 0x8000000000000000ull;
-  const bool even = (q & 1) == 0;
-  sn = __longlong_as_double((long long)((unsigned long long)__double_as_longlong(even ? sinr : cosr) ^ xsgn ^ sgn_hi));
-  cs = __longlong_as_double((long long)((unsigned long long)__double_as_longlong(even ? cosr : -sinr) ^ sgn_hi));
-  // __ocmlpriv_tanred2_f64(rh, rl, q & 1)
-  const double h2 = rh * rh;
-  const double h2l = fma(rh, rh, -h2);
-  const double s = h2 + fma(rh, rl * 2.0, h2l);
-  double z = fma3(s, bits_f64(0x3EF5E089C751C08Cull), bits_f64(0xBF078809A9A29F71ull));
-  z = fma3(s, z, bits_f64(0x3F17746F90A8AAE0ull));
-  z = fma3(s, z, bits_f64(0xBEFBB44DA6FBF144ull));
-  z = fma3(s, z, bits_f64(0x3F21E634A7943ACFull));
-  z = fma3(s, z, bits_f64(0x3F2D250FDEB68FEBull));
-  z = fma3(s, z, bits_f64(0x3F437FD9B58C4D95ull));
-  z = fma3(s, z, bits_f64(0x3F57D5AF15120E2Cull));
-  z = fma3(s, z, bits_f64(0x3F6D6D93E09491DFull));
-  z = fma3(s, z, bits_f64(0x3F8226E12033784Dull));
-  z = fma3(s, z, bits_f64(0x3F9664F49AC36AE2ull));
-  z = fma3(s, z, bits_f64(0x3FABA1BA1B451C21ull));
-  z = fma3(s, z, bits_f64(0x3FC11111111185B7ull));
-  z = fma3(s, z, bits_f64(0x3FD55555555554EEull));
-  const double w = s * z;
-  const double v = rh * w;
-  const double vl = fma(rh, w, -v);
-  const double th0 = rh + v;
-  const double vt = v - (th0 - rh);
-  const double tl0 = (rl + vl) + vt;
-  const double th = th0 + tl0;                // tan(reduced), head
-  const double tl = tl0 - (th - th0);         // and tail
-  double rc = __builtin_amdgcn_rcp(th);
-  rc = fma(fma(-th, rc, 1.0), rc, rc);
-  rc = fma(fma(-th, rc, 1.0), rc, rc);
-  const double pr = th * rc;
-  const double pe = fma(rc, tl, fma(rc, th, -pr));
-  const double ps = pr + pe;
-  const double pt = pe - (ps - pr);
-  const double o1 = 1.0 - ps;
-  const double o2 = ((1.0 - o1) - ps) - pt;
-  const double ncot = rc + rc * (o1 + o2);    // 1 / tan(reduced)
-  const double tr = ((q & 1) == 0) ? th : -ncot;
-  tn = __longlong_as_double((long long)((unsigned long long)__double_as_longlong(tr) ^ xsgn));
+  rwrt_math::rm_sincostan_small(x, sn, cs, tn);
 }
 
 // Mercator factors of cal_bs_mercator_point (bs.py:856-860).
@@ -1162,7 +1096,7 @@ __device__ __forceinline__ double initial_step(const P& fun, double t0, const do
     h1 = np_max(1e-6, h0 * 1e-3);
   } else {
     const double dm = (d1 != d1) ? d2 : ((d2 != d2) ? d1 : (d1 >= d2 ? d1 : d2));  // nanmax
-    h1 = pow(0.01 / dm, 0.2);
+    h1 = rm_pow(0.01 / dm, 0.2);
   }
   return np_min(100.0 * h0, h1);
 }
@@ -1214,7 +1148,7 @@ struct Lane {
 #if RWRT_DIAG_NOPOW
       double fac = np_min(kMaxFactor, kSafety / (0.5 + en));
 #else
-      double fac = np_min(kMaxFactor, kSafety * pow(en, kErrExp));
+      double fac = np_min(kMaxFactor, kSafety * rm_pow(en, kErrExp));
 #endif
       if (en == 0.0) fac = kMaxFactor;
       if (rejected) fac = np_min(1.0, fac);
@@ -1232,7 +1166,7 @@ struct Lane {
 #if RWRT_DIAG_NOPOW
     hs = ha * np_max(kMinFactor, kSafety / (0.5 + en));
 #else
-    hs = ha * np_max(kMinFactor, kSafety * pow(en, kErrExp));
+    hs = ha * np_max(kMinFactor, kSafety * rm_pow(en, kErrExp));
 #endif
     rejected = true;
     ++nrej;
@@ -1546,6 +1480,9 @@ __global__ void math_kernel(int kind, int64_t n, const double* __restrict__ x,
     case 17: { double sn, cs, tn; sincostan(a, sn, cs, tn); r = sn; } break;
     case 18: { double sn, cs, tn; sincostan(a, sn, cs, tn); r = cs; } break;
     case 19: { double sn, cs, tn; sincostan(a, sn, cs, tn); r = tn; } break;
+    case 20: r = rm_pow(a, b); break;
+    case 21: r = rwrt_math::rm_exp(a); break;
+    case 22: r = recip2(a); break;
     default: r = fmod_pos(a, b); break;
   }
   out[i] = r;
@@ -2245,7 +2182,7 @@ rwrt_status rwrt_kat_rk45(int32_t kind, int64_t ncol, const double* d_y0, int32_
 
 rwrt_status rwrt_selftest_math(int32_t kind, int64_t n, const double* d_x, const double* d_y,
                                double* d_out, void* stream) {
-  if (n < 0 || kind < 0 || kind > 19 || (n > 0 && (!d_x || !d_out)))
+  if (n < 0 || kind < 0 || kind > 22 || (n > 0 && (!d_x || !d_out)))
     return fail(RWRT_ERR_ARG, "bad selftest arguments%s");
   if (n == 0) return RWRT_OK;
   hipLaunchKernelGGL(math_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, kind,
