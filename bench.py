@@ -166,8 +166,11 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
+        # one GPU per rank; RWRT_DIST_BACKEND=gloo with fewer GPUs than ranks
+        # is the single-GPU rehearsal of this path (ranks share a device)
+        local = local % max(torch.cuda.device_count(), 1)
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group(os.environ.get("RWRT_DIST_BACKEND", "nccl"))
     dev = torch.device("cuda", local if world > 1 else 0)
 
     if args.config == "C5":
