@@ -607,6 +607,82 @@ __device__ __forceinline__ void lookup_end(const CachedVaryingBG32& B,
   B.end(p, g);
 }
 
+// VaryingBG<double> with the per-lane LDS cache holding ONE level: the lower
+// bracketing level's four fp64 corner records (4 x 96 B = the static cache's
+// 24 chunks), keyed by (cell, level pair); the upper level is gathered from
+// global memory in end().  Both levels of fp64 corners (768 B per lane) would
+// not fit next to the stages; caching one halves the gathers of every
+// evaluation that stays in its cell.  Same values, same blend as
+// VaryingBG<double>::interp11.
+struct CachedVaryingBG64 {
+  static constexpr bool kTimeVarying = true;
+  VaryingBG<double> V;
+  char* wave_base;
+  unsigned lane16;
+  mutable unsigned key_x, key_y;
+  mutable int key_j;
+
+  struct Pending {
+    double w[4];
+    double wt;
+    unsigned o[4];
+    const double* B;
+  };
+  __device__ __forceinline__ const double2& chunk(int j, int q) const {
+    return *reinterpret_cast<const double2*>(wave_base + (j * 6 + q) * 1024 + lane16);
+  }
+  __device__ __forceinline__ Pending begin(double lon, double lat, double t) const {
+    Pending p;
+    unsigned kx, ky;
+    int jl;
+    V.cell(lon, lat, p.o, p.w, kx, ky);
+    const double* A = V.level(t, p.wt, jl);
+    if (kx != key_x || ky != key_y || jl != key_j) {   // miss: refill by LDS-DMA
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int q = 0; q < 6; ++q)
+          __builtin_amdgcn_global_load_lds((global_void_ptr)(A + p.o[j] + 2 * q),
+                                           (lds_void_ptr)(wave_base + (j * 6 + q) * 1024), 16, 0, 0);
+      key_x = kx;
+      key_y = ky;
+      key_j = jl;
+    }
+    p.B = A + (V.nlev > 1 ? V.lev_stride : 0);
+    return p;
+  }
+  __device__ __forceinline__ void end(const Pending& p, double g[11]) const {
+    double gb[11];
+    V.blend_level<11>(p.B, p.o, p.w, 0, gb);
+    double2 v[4][6];
+#pragma unroll
+    for (int q = 0; q < 6; ++q)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j][q] = chunk(j, q);
+    __builtin_amdgcn_sched_barrier(0);
+    double ga[11];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      ga[2 * q] = VaryingBG<double>::bl(p.w, v[0][q].x, v[1][q].x, v[2][q].x, v[3][q].x);
+      if (2 * q + 1 < 11) ga[2 * q + 1] = VaryingBG<double>::bl(p.w, v[0][q].y, v[1][q].y, v[2][q].y, v[3][q].y);
+    }
+#pragma unroll
+    for (int i = 0; i < 11; ++i) g[i] = ga[i] * (1.0 - p.wt) + gb[i] * p.wt;
+  }
+  __device__ __forceinline__ void interp4(double lon, double lat, double t, double& fu, double& fv,
+                                          double& fqx, double& fqy) const {
+    V.interp4(lon, lat, t, fu, fv, fqx, fqy);
+  }
+};
+__device__ __forceinline__ CachedVaryingBG64::Pending lookup_begin(const CachedVaryingBG64& B, double lon,
+                                                                   double lat, double t) {
+  return B.begin(lon, lat, t);
+}
+__device__ __forceinline__ void lookup_end(const CachedVaryingBG64& B,
+                                           const CachedVaryingBG64::Pending& p, double g[11]) {
+  B.end(p, g);
+}
+
 // The background a persistent lane integrates with: the cached lookup for the
 // static state (kernel-owned LDS), the plain one otherwise.
 template <class BG>
@@ -634,6 +710,20 @@ struct LaneBG<VaryingBG<float>> {
     return CachedVaryingBG32{B, lds + wave * kCacheBytesPerWave, (threadIdx.x & 63u) * 16u, ~0u, ~0u, -1};
   }
 };
+#ifndef RWRT_CACHE_FP64_LEVELS
+#define RWRT_CACHE_FP64_LEVELS 1
+#endif
+#if RWRT_CACHE_FP64_LEVELS
+template <>
+struct LaneBG<VaryingBG<double>> {
+  using type = CachedVaryingBG64;
+  static constexpr int kLdsBytes = 4 * kCacheBytesPerWave;
+  __device__ static CachedVaryingBG64 make(const VaryingBG<double>& B, char* lds) {
+    const unsigned wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    return CachedVaryingBG64{B, lds + wave * kCacheBytesPerWave, (threadIdx.x & 63u) * 16u, ~0u, ~0u, -1};
+  }
+};
+#endif
 #endif
 
 // ---------------------------------------------------------------------------

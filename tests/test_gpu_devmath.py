@@ -123,3 +123,30 @@ def test_rk4_c2_90d_bitwise_with_device_math(kind):
     nt = int(g["nt"])
     hist = run_wr(kind, "C2", nt, "")
     check_rows(row_hashes(hist), g["rk4_row_sha"], hist, g["rk4_last"])
+
+
+@pytest.mark.parametrize("fp32", [False, True])
+def test_time_varying_c2_bitwise_with_device_math(fp32):
+    """The time-varying path (fp64 levels: one level in the LDS cache, the
+    other gathered; fp32 levels: both cached) over 2 days -- past the last
+    level, where the time weight clips -- equals the oracle bit for bit."""
+    import torch
+    import rwrt_oracle as O
+    import synthetic as S
+    from test_gpu_time_varying import tv
+    eng, ob, ob0 = tv(fp32)
+    cfg = S.config("C2")
+    slon, slat = O.source_matrix(cfg.SW_lon, cfg.SW_lat, cfg.dlon, cfg.dlat, cfg.nnx, cfg.nny)
+    rows = eng.initial_rows(slon, slat, cfg.zwn, cfg.freq).cpu().numpy()
+    y0 = rows[:5].reshape(5, -1)
+    nt = 25
+    got = {}
+    res = eng.integrate(torch.as_tensor(y0), nt, 7200.0, ttotal=(nt - 1) * 7200.0,
+                        sink=lambda a, b, o: got.__setitem__(a, o.cpu().numpy().copy()))
+    hist = np.concatenate([got[k] for k in sorted(got)], axis=1)       # rows 1..nt-1
+    with np.errstate(all="ignore"), O.device_math():
+        ref, nacc, _, st = O.ray_run(ob, y0.copy(), nt, 7200.0)
+    assert st == 0
+    g = np.transpose(hist[:, :, :7], (2, 1, 0))
+    assert same(g, ref[:, 1:]), int((~((g == ref[:, 1:]) | (np.isnan(g) & np.isnan(ref[:, 1:])))).sum())
+    assert np.array_equal(res.nacc.cpu().numpy(), nacc)
