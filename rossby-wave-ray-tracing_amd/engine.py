@@ -291,11 +291,10 @@ class RayEngine:
         order = torch.sort((~live).to(torch.int8), stable=True).indices.to(torch.int64).contiguous()
         chunk = chunk or (nt - 1)
         rows_max = min(chunk, nt - 1)
-        if out is None or out.numel() < nray * rows_max * H.NOUT:
-            out = torch.empty((nray, rows_max, H.NOUT), dtype=F64, device=self.device)
-        flat = out.reshape(-1)
-        for i0 in range(1, nt, chunk):
+        bufs = _row_buffers(out, nray, rows_max, self.device)
+        for k, i0 in enumerate(range(1, nt, chunk)):
             i1 = min(i0 + chunk, nt)
+            flat = bufs[k % len(bufs)].reshape(-1)
             view = flat[: nray * (i1 - i0) * H.NOUT].view(nray, i1 - i0, H.NOUT)
             if events is not None:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -363,10 +362,9 @@ class RayEngine:
             i0 = bounds[-1][1]
         rows_max = max(b - a for a, b in bounds)
         prev_work = None
-        if out is None or out.shape[0] != nray or out.shape[1] * out.shape[2] < rows_max * H.NOUT:
-            out = torch.empty((nray, rows_max, H.NOUT), dtype=F64, device=self.device)
-        flat = out.view(-1)
-        for i0, i1 in bounds:
+        bufs = _row_buffers(out, nray, rows_max, self.device)
+        for k, (i0, i1) in enumerate(bounds):
+            flat = bufs[k % len(bufs)].view(-1)
             view = flat[: nray * (i1 - i0) * H.NOUT].view(nray, i1 - i0, H.NOUT)
             n_heavy = 0
             if order_policy in ("cost", "priority") and prev_work is not None:
@@ -392,6 +390,18 @@ class RayEngine:
         res = RunResult(cnt[:, 0], cnt[:, 1], st["nanrow"], False, brk, n_live)
         res.bounds = bounds
         return res
+
+
+def _row_buffers(out, nray, rows_max, device):
+    """The device row buffers chunks are written to: ``out`` (one tensor, or a
+    list whose buffers alternate so that a consumer can read chunk k while
+    chunk k+1 is computed, hostio.HistorySink), each ``[nray][>= rows][8]``;
+    allocated when missing or too small."""
+    bufs = list(out) if isinstance(out, (list, tuple)) else [out]
+    for j, b in enumerate(bufs):
+        if b is None or b.numel() < nray * rows_max * H.NOUT:
+            bufs[j] = torch.empty((nray, rows_max, H.NOUT), dtype=F64, device=device)
+    return bufs
 
 
 def ctypes_ref(p):

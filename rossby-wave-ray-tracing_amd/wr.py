@@ -189,14 +189,27 @@ class WR:
 
         chunk = self.chunk_rows or _default_chunk(nray, self.nt)
         grp = group if world > 1 else None
-        if method == "rk4":
-            res = eng.integrate_rk4(torch.as_tensor(y0[:, idx]), self.nt, float(self.tstep[0]),
+        out, hs = None, None
+        if world == 1:
+            # single GPU: chunks reach the host arrays while the next one is
+            # computed (permute on the device, pinned D2H, threaded copies)
+            from hostio import HistorySink
+            hs = HistorySink(hist, rows_shape, nray, min(chunk, self.nt - 1), eng.device,
+                             progress=(lambda i: progress_bar(i, self.nt)) if self.progress else None)
+            sink, out = hs, hs.buffers()
+        try:
+            if method == "rk4":
+                res = eng.integrate_rk4(torch.as_tensor(y0[:, idx]), self.nt, float(self.tstep[0]),
+                                        chunk=chunk, sink=sink, cut_rad=float(self.cut_off[0]),
+                                        group=grp, out=out)
+            else:
+                res = eng.integrate(torch.as_tensor(y0[:, idx]), self.nt, float(self.tstep[0]),
+                                    self.rtol, self.atol, self.MinStepFactor, ttotal=self.ttotal,
                                     chunk=chunk, sink=sink, cut_rad=float(self.cut_off[0]),
-                                    group=grp)
-        else:
-            res = eng.integrate(torch.as_tensor(y0[:, idx]), self.nt, float(self.tstep[0]),
-                                self.rtol, self.atol, self.MinStepFactor, ttotal=self.ttotal,
-                                chunk=chunk, sink=sink, cut_rad=float(self.cut_off[0]), group=grp)
+                                    group=grp, out=out)
+        finally:
+            if hs is not None:
+                hs.finish()
         if res.break_row is not None:
             for h in hist:
                 h[res.break_row:] = np.nan     # rows never stored (wr.py:853-855, 886-887)

@@ -462,3 +462,37 @@ def test_rk4_c1_90d():
     d = d.max(axis=1)
     assert d[:361].max() <= 1e-8, d[:361].max()
     assert d.max() <= 2 * floor90, (d.max(), floor90)
+
+
+# ------------------------------------------------------------ drop-in delivery
+@pytest.mark.parametrize("inte_method", ["rk45", ""])
+def test_dropin_history_matches_engine_rows(inte_method):
+    """WR.ray_run(mode='hip') delivers every chunk into rlon..rvg through
+    hostio.HistorySink (alternating device buffers, copy stream, pinned
+    staging, threaded host copies): with 7-row chunks over 3 days the host
+    arrays equal the rows of one unchunked engine run bit for bit."""
+    from wr import WR
+    cfg = S.config("C2")
+    bs = bs_of("nonzonal")
+    nt = 37
+    w = WR(cfg.nzwn, cfg.nsource, 7200.0, (nt - 1) * 7200.0, cfg.freq, nx=bs.nlon, ny=bs.nlat,
+           chunk_rows=7)
+    w.bs = bs
+    w.set_zwn(cfg.zwn)
+    w.set_source_matrix(cfg.SW_lon, cfg.SW_lat, cfg.dlon, cfg.dlat, cfg.nnx, cfg.nny)
+    with np.errstate(all="ignore"):
+        w.ray_run(mode="hip", inte_method=inte_method)
+    got = np.array([w.rlon, w.rlat, w.rzwn, w.rmwn, w.ramp, w.rug, w.rvg]).reshape(7, nt, -1)
+    y0 = torch.as_tensor(got[:5, 0])
+    eng = bs.engine()
+    if inte_method == "rk45":
+        out = torch.empty((y0.shape[1], nt - 1, 8), dtype=torch.float64, device="cuda")
+        eng.integrate(y0, nt, 7200.0, w.rtol, w.atol, w.MinStepFactor, ttotal=(nt - 1) * 7200.0,
+                      out=out, cut_rad=float(w.cut_off[0]))
+    else:
+        out = torch.empty((y0.shape[1], nt - 1, 8), dtype=torch.float64, device="cuda")
+        eng.integrate_rk4(y0, nt, 7200.0, out=out, cut_rad=float(w.cut_off[0]))
+    want = out[:, :, :7].permute(2, 1, 0).cpu().numpy()
+    a, b = got[:, 1:], want
+    assert np.array_equal(np.where(np.isnan(a), np.nan, a).view(np.int64),
+                          np.where(np.isnan(b), np.nan, b).view(np.int64))
