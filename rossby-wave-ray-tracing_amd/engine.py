@@ -336,6 +336,7 @@ class RayEngine:
         tb = torch.as_tensor(t_eval_of(nt, tstep, ttotal), dtype=F64, device=self.device)
         st = self.init(y0, p)
         summary = st["summary"]
+        n_live_local = int(summary[0].item())   # this rank's shard (the queue bound)
         if group is not None:
             from shard import reduce_summary
             summary = reduce_summary(summary, group)
@@ -370,7 +371,7 @@ class RayEngine:
             if order_policy in ("cost", "priority") and prev_work is not None:
                 order = self.cost_order(st, cnt.sum(1) - prev_work)
                 if order_policy == "priority":
-                    n_heavy = min(self.heavy_lanes(), n_live)
+                    n_heavy = min(self.heavy_lanes(), n_live_local)
             prev_work = cnt.sum(1)
             if events is not None:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

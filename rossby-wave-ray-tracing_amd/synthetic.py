@@ -32,10 +32,15 @@ def background(kind="zonal", res=2.5):
     coslat = np.cos(np.deg2rad(phi))
     u = jets * coslat * np.ones_like(lam)
     v = np.zeros_like(u)
-    if kind == "nonzonal":
+    if kind == "superrotation":
+        # solid-body super-rotation U = U0 cos(phi), V = 0 (U0 = 15 m/s): the
+        # docs' Great-Circle example (Hoskins & Karoly 1981), whose
+        # stationary rays follow great circles
+        u = 15.0 * coslat * np.ones_like(lam)
+    elif kind == "nonzonal":
         u = u * (1.0 + 0.3 * np.cos(np.deg2rad(lam - 140.0)))
         v = 4.0 * np.sin(3.0 * np.deg2rad(lam)) * coslat ** 2
-    elif kind != "zonal":
+    elif kind not in ("zonal", "superrotation"):
         raise ValueError(f"unknown background kind {kind!r}")
     return dict(u=u.astype(np.float32), v=v.astype(np.float32), lat=lat, lon=lon)
 
