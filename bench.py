@@ -89,6 +89,25 @@ def cpu_baseline(bg, y0, nrays, days, seed=0):
     return pick, hist, int(nacc.sum()), dt, nt
 
 
+def cpu_baseline_mp(bg, y0, procs, rays_per_proc, days, seed=1):
+    """The oracle on ``procs`` host processes (rays are independent), each on
+    its own ``rays_per_proc`` live C3 rays for ``days``; rate = all accepted
+    steps / the slowest process's ray-loop time."""
+    import multiprocessing as mp
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import rwrt_oracle as O
+    rng = np.random.default_rng(seed)
+    live = np.where(~np.isnan(y0.mean(axis=0)))[0]
+    pick = rng.choice(live, size=min(procs * rays_per_proc, len(live)), replace=False)
+    nt = int(round(days * 12)) + 1
+    jobs = [(bg, y0[:, part].copy(), nt, 7200.0) for part in np.array_split(pick, procs)]
+    with mp.get_context("spawn").Pool(procs) as pool:
+        res = pool.map(O.ray_run_timed, jobs)
+    steps = sum(r[0] for r in res)
+    wall = max(r[1] for r in res)
+    return steps, wall, len(pick)
+
+
 def devmath_check(bg, y0, pick, gpu, nt, nrays=2048):
     """Bit-identity of the GPU rows with the oracle run on the device's own
     sin/cos/tan/pow (rwrt_oracle.device_math(), tests/test_gpu_devmath.py):
@@ -137,6 +156,8 @@ def main():
     ap.add_argument("--cpu-rays", type=int, default=16384)
     ap.add_argument("--cpu-days", type=float, default=4.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-procs", type=int, default=16,
+                    help="processes of the multi-core CPU baseline (1: skip it)")
     ap.add_argument("--periods", type=int, default=5, help="C3 periods in the batch (1-5)")
     ap.add_argument("--order", default="priority", choices=["priority", "cost", "live"],
                     help="work-queue order: heaviest rays to high-priority waves (priority), "
@@ -290,6 +311,14 @@ def main():
                 "sample": f"{len(pick)} live C3 rays x {args.cpu_days:g} d ({csteps} ray-steps, "
                           f"{cdt:.1f} s) with oracle/rwrt_oracle.py (NumPy, bit-exact vs reference)",
                 "host_cpus": os.cpu_count()}
+            if args.cpu_procs > 1:
+                msteps, mwall, mrays = cpu_baseline_mp(bg, y0, args.cpu_procs, args.cpu_rays // 4,
+                                                       args.cpu_days)
+                result["cpu_baseline_mp"] = {
+                    "value": msteps / mwall, "unit": "ray-steps/s", "cores": args.cpu_procs,
+                    "kind": "port",
+                    "sample": f"{mrays} live C3 rays x {args.cpu_days:g} d over {args.cpu_procs} "
+                              f"processes ({msteps} ray-steps, slowest process {mwall:.1f} s)"}
             # parity of the same sample on the GPU after the same horizon
             rows = {}
             eng.integrate(torch.as_tensor(y0[:, pick], device=dev), cnt, 7200.0,

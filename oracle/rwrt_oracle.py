@@ -736,3 +736,16 @@ def run_config_rk4(bg, cfg, nt=None):
         nt = int(cfg.ttotal * DAY / tstep) + 1
     row0 = np.array(rows).reshape(7, -1)
     return ray_run_rk4(bg, row0[:5].copy(), nt, tstep, row0=row0)
+
+
+def ray_run_timed(args):
+    """``(bg_kwargs, y0, nt, tstep)`` -> (accepted steps, seconds in ray_run):
+    one process of bench.py's multi-core CPU baseline (picklable, imports
+    nothing beyond this module)."""
+    import time
+    bg_kwargs, y0, nt, tstep = args
+    bg = Background(**bg_kwargs)
+    t0 = time.perf_counter()
+    with np.errstate(all="ignore"):
+        _, nacc, _, _ = ray_run(bg, y0, nt, tstep)
+    return int(nacc.sum()), time.perf_counter() - t0
