@@ -351,6 +351,24 @@ constexpr int kCacheBytesPerWave = kCacheChunks * 64 * 16;  // 24 KiB
 typedef __attribute__((address_space(3))) void* lds_void_ptr;
 typedef __attribute__((address_space(1))) const void* global_void_ptr;
 
+// The LDS destination (M0) of LDS-DMA chunk k of a refill: the wave's slice
+// base passed through an opaque SGPR copy, so that the compiler rebuilds the
+// 24 destinations with one s_add each instead of keeping 24 loop-invariant
+// M0 values live (they spill to VGPR lanes: v_readlane + s_mov per load).
+#ifndef RWRT_FRESH_M0
+#define RWRT_FRESH_M0 1
+#endif
+__device__ __forceinline__ char* lds_slice_base(char* wave_base) {
+#if RWRT_FRESH_M0
+  typedef __attribute__((address_space(3))) char lds_char;
+  unsigned b = (unsigned)(size_t)(lds_char*)wave_base;
+  asm volatile("" : "+s"(b));
+  return (char*)(lds_char*)(size_t)b;
+#else
+  return wave_base;
+#endif
+}
+
 struct CachedStaticBG {
   static constexpr bool kTimeVarying = false;
   Field F;
@@ -368,12 +386,13 @@ struct CachedStaticBG {
     const Corners k = corners(F, py_mod_2pi(lon), lat);
     if (k.key_x != key_x || k.key_y != key_y) {   // miss: refill the slice by LDS-DMA
       const double* src[4] = {k.a, k.b, k.c, k.d};
+      char* const base = lds_slice_base(wave_base);
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int q = 0; q < 6; ++q)
           __builtin_amdgcn_global_load_lds((global_void_ptr)(src[j] + 2 * q),
-                                           (lds_void_ptr)(wave_base + (j * 6 + q) * 1024), 16, 0, 0);
+                                           (lds_void_ptr)(base + (j * 6 + q) * 1024), 16, 0, 0);
       key_x = k.key_x;
       key_y = k.key_y;
     }
@@ -555,6 +574,7 @@ struct CachedVaryingBG32 {
     const float* A = V.level(t, p.wt, jl);
     if (kx != key_x || ky != key_y || jl != key_j) {   // miss: refill by LDS-DMA
       const float* L[2] = {A, A + (V.nlev > 1 ? V.lev_stride : 0)};
+      char* const base = lds_slice_base(wave_base);
 #pragma unroll
       for (int lev = 0; lev < 2; ++lev)
 #pragma unroll
@@ -562,7 +582,7 @@ struct CachedVaryingBG32 {
 #pragma unroll
           for (int q = 0; q < 3; ++q)
             __builtin_amdgcn_global_load_lds((global_void_ptr)(L[lev] + o[j] + 4 * q),
-                                             (lds_void_ptr)(wave_base + ((lev * 4 + j) * 3 + q) * 1024),
+                                             (lds_void_ptr)(base + ((lev * 4 + j) * 3 + q) * 1024),
                                              16, 0, 0);
       key_x = kx;
       key_y = ky;
@@ -638,12 +658,13 @@ struct CachedVaryingBG64 {
     V.cell(lon, lat, p.o, p.w, kx, ky);
     const double* A = V.level(t, p.wt, jl);
     if (kx != key_x || ky != key_y || jl != key_j) {   // miss: refill by LDS-DMA
+      char* const base = lds_slice_base(wave_base);
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int q = 0; q < 6; ++q)
           __builtin_amdgcn_global_load_lds((global_void_ptr)(A + p.o[j] + 2 * q),
-                                           (lds_void_ptr)(wave_base + (j * 6 + q) * 1024), 16, 0, 0);
+                                           (lds_void_ptr)(base + (j * 6 + q) * 1024), 16, 0, 0);
       key_x = kx;
       key_y = ky;
       key_j = jl;
