@@ -41,7 +41,16 @@ constexpr double kRInv = 1.0 / 6.3712e6;   // RN(1 / R)
 // A zero x stays on the fast path (q0 = x * RN(1/R) is the correctly signed
 // zero, kept by the copysign): in a zonal flow dk/dt is exactly -0 for every
 // ray, so the fallback would otherwise run on every evaluation.
+#ifndef RWRT_RHS_TRIG_SMALL
+#define RWRT_RHS_TRIG_SMALL 1
+#endif
+#ifndef RWRT_DIV_REARTH_IEEE
+#define RWRT_DIV_REARTH_IEEE 1
+#endif
 __device__ __forceinline__ double div_rearth(double x) {
+#if RWRT_DIV_REARTH_IEEE
+  return x / kREarth;
+#endif
   const double ax = fabs(x);
   const double q0 = x * kRInv;
   const double r = fma(-q0, kREarth, x);
@@ -106,10 +115,12 @@ __device__ __forceinline__ double fmod_pos(double a, double b, double binv = 0.0
   double r = fma(-n, b, x);
   const double lo = r + b, hi = fma(-(n + 1.0), b, x);
   r = (r < 0.0) ? lo : ((r >= b) ? hi : r);
+#if !RWRT_DIAG_FMOD_NOFALLBACK
   if (!(x < 0x1p40)) {
     asm volatile("");   // NaN, inf, huge: library routine (rare branch)
     r = fabs(fmod(a, b));
   }
+#endif
   return copysign(r, a);
 }
 
@@ -177,8 +188,15 @@ __device__ __forceinline__ double div_hw(double a, double b, double rb) {
 }
 // x / c for a wave-uniform c: the reciprocal is loop-invariant (hoisted to
 // the kernel entry)
+#ifndef RWRT_CELL_DIV_IEEE
+#define RWRT_CELL_DIV_IEEE 1
+#endif
 __device__ __forceinline__ double div_uniform(double x, double c) {
+#if RWRT_CELL_DIV_IEEE
+  return x / c;
+#else
   return div_hw(x, c, recip_hw(c));
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -883,7 +901,14 @@ __device__ __forceinline__ void ray_rhs(const BG& B, double t, const double* y, 
   const double tn = tan(lat);
 #else
   double tn;
+#if RWRT_RHS_TRIG_SMALL
+  // |lat| >= 2^30, inf or NaN: the ray is masked (|lat| >= pi/2) or its
+  // lookup is NaN, so every output is NaN whatever s, c, tn are -- no
+  // library fallback needed here
+  rwrt_math::rm_sincostan_small(lat, s, c, tn);
+#else
   sincostan(lat, s, c, tn);         // == sin(), cos(), tan(), one reduction
+#endif
 #endif
 #endif
 #if RWRT_DIAG_NOINTERP   // timing-only diagnostic build: constant background
