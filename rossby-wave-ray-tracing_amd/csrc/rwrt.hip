@@ -1280,33 +1280,34 @@ struct Lane {
     double en = dp54_attempt(fun, K, t, y, f, h, rtol, atol, yn, k6, nullptr, 0,
                              P::NAUX > 0 ? aux : nullptr);
     if (en != en) en = 0.0;                 // rkf45.py:446
-    if (en < 1.0) {
 #if RWRT_DIAG_NOPOW
-      double fac = np_min(kMaxFactor, kSafety / (0.5 + en));
+    const double sp = kSafety / (0.5 + en);
 #else
-      double fac = np_min(kMaxFactor, kSafety * rm_pow(en, kErrExp));
+    // SAFETY * error_norm ** (-1/5), shared by the accept (rkf45.py:453-469) and
+    // reject (rkf45.py:471-475) factors: one pow per attempt even when the
+    // wave's lanes split between the two outcomes
+    const double sp = kSafety * rm_pow(en, kErrExp);
 #endif
-      if (en == 0.0) fac = kMaxFactor;
-      if (rejected) fac = np_min(1.0, fac);
-      habs = ha * fac;
-      t = (tn != tn) ? tb : tn;             // rkf45.py:503
+    // Accept / reject as selects: the lanes of a wave usually disagree, and
+    // a branch pair would execute both sides anyway.
+    const bool acc = en < 1.0;
+    double fac = np_min(kMaxFactor, sp);
+    if (en == 0.0) fac = kMaxFactor;
+    if (rejected) fac = np_min(1.0, fac);
+    const double tnew = (tn != tn) ? tb : tn;              // rkf45.py:503
+    habs = acc ? ha * fac : habs;
+    hs = acc ? hs : ha * np_max(kMinFactor, sp);
+    t = acc ? tnew : t;
 #pragma unroll
-      for (int v = 0; v < NV; ++v) {
-        y[v] = yn[v];
-        f[v] = k6[v];
-      }
-      in_step = false;
-      ++nacc;
-      return (t - tb >= 0.0) ? kReached : kStep;   // rkf45.py:250
+    for (int v = 0; v < NV; ++v) {
+      y[v] = acc ? yn[v] : y[v];
+      f[v] = acc ? k6[v] : f[v];
     }
-#if RWRT_DIAG_NOPOW
-    hs = ha * np_max(kMinFactor, kSafety / (0.5 + en));
-#else
-    hs = ha * np_max(kMinFactor, kSafety * rm_pow(en, kErrExp));
-#endif
-    rejected = true;
-    ++nrej;
-    return kStep;
+    in_step = !acc;
+    rejected = rejected || !acc;
+    nacc += acc ? 1 : 0;
+    nrej += acc ? 0 : 1;
+    return (acc && t - tb >= 0.0) ? kReached : kStep;   // rkf45.py:250
   }
 };
 
