@@ -977,11 +977,30 @@ __device__ __forceinline__ double cal_dis_c(double lon_c, double lat_c, double l
 }
 // cal_dis_c(...) >= cut_off, with the atan2 skipped when the haversine
 // argument is certainly below the threshold (cut_a: haversine_cut on the host)
+// sin() of two arguments through the one-reduction routine (== sin() for
+// |x| < 2^30), with one shared fallback branch to the library for the rest
+__device__ __forceinline__ void sin2(double a, double b, double& sa, double& sb) {
+  double c, t;
+  rwrt_math::rm_sincostan_small(a, sa, c, t);
+  rwrt_math::rm_sincostan_small(b, sb, c, t);
+  if (!(fabs(a) < 0x1p30 && fabs(b) < 0x1p30)) {
+    asm volatile("");   // huge, infinite or NaN: library routines (rare branch)
+    sa = sin(a);
+    sb = sin(b);
+  }
+}
+// cos() through the one-reduction routine for an argument known to be below
+// pi/2 in magnitude or NaN (no fallback needed: NaN -> NaN)
+__device__ __forceinline__ double cos_small(double x) {
+  double sn, cs, tn;
+  rwrt_math::rm_sincostan_small(x, sn, cs, tn);
+  return cs;
+}
 __device__ __forceinline__ bool cal_dis_reaches(double lon_c, double lat_c, double lon_p,
                                                 double lat_p, double cos_c, double cos_p,
                                                 double cut_off, double cut_a) {
-  const double sd = sin((lat_c - lat_p) / 2.0);
-  const double sl = sin((lon_c - lon_p) / 2.0);
+  double sd, sl;
+  sin2((lat_c - lat_p) / 2.0, (lon_c - lon_p) / 2.0, sd, sl);
   const double a = sd * sd + (cos_p * cos_c) * (sl * sl);
   bool r = false;
   if (!(a < cut_a)) {
@@ -1537,7 +1556,7 @@ __global__ void __launch_bounds__(256, RWRT_WAVES_PER_SIMD) rk45_run_kernel(RunA
     double ug, vg, cos_c = kNaN;
     bool masked = fabs(y[1]) >= kHalfPi;
     if (!masked) {
-      cos_c = have ? L.aux[2] : cos(y[1]);
+      cos_c = have ? L.aux[2] : cos_small(y[1]);   // |y[1]| < pi/2 or NaN here
 #if RWRT_DIAG_NOPOST
       masked = fabs(y[1] - prev_lat) >= a.cut_off;
 #else
@@ -1562,12 +1581,22 @@ __global__ void __launch_bounds__(256, RWRT_WAVES_PER_SIMD) rk45_run_kernel(RunA
     // masks against itself is a no-op), so every remaining row of the chunk
     // equals this one: write them all and release the lane.
     const int last = (st == Lane<RayProblem, KStore>::kFrozen) ? a.it_end : it + 1;
-    for (int k = it; k < last; ++k) {
-      double2* o = reinterpret_cast<double2*>(a.out + ((size_t)ray * nrows + (k - a.it_begin)) * RWRT_NOUT);
+    {
+      double2* o = reinterpret_cast<double2*>(a.out + ((size_t)ray * nrows + (it - a.it_begin)) * RWRT_NOUT);
       o[0] = r0;
       o[1] = r1;
       o[2] = r2;
       o[3] = r3;
+    }
+    if (last > it + 1) {
+      asm volatile("");   // frozen: the remaining rows of the chunk (rare branch)
+      for (int k = it + 1; k < last; ++k) {
+        double2* o = reinterpret_cast<double2*>(a.out + ((size_t)ray * nrows + (k - a.it_begin)) * RWRT_NOUT);
+        o[0] = r0;
+        o[1] = r1;
+        o[2] = r2;
+        o[3] = r3;
+      }
     }
     if (nanrow == a.nt && isnan(y[0])) nanrow = it;  // wr.py:853-855 (host reduces)
     prev_lon = y[0];
