@@ -230,7 +230,8 @@ rwrt_status rwrt_kat_rk45(int32_t kind, int64_t ncol, const double* d_y0,
  * 15 x / y by a shared reciprocal, 16 np.floor(x).astype(int32),
  * 17/18/19 sin/cos/tan from the fused one-reduction routine, 20 pow(x, y) and
  * 21 exp(x) as restated in csrc/rwrt_math.h, 22 the refined reciprocal
- * (v_rcp_f64 + two Newton steps) of x.
+ * (v_rcp_f64 + two Newton steps) of x, 23/24 x / y through the interleaved
+ * division pair (as its first / second quotient).
  * Lets the tests prove which operations are bit-exact on the GPU (IEEE
  * division, sqrt, fmod) and measure the last-bit agreement of the rest. */
 rwrt_status rwrt_selftest_math(int32_t kind, int64_t n, const double* d_x,

@@ -62,6 +62,57 @@ __device__ __forceinline__ double div_rearth(double x) {
   return q;
 }
 constexpr double kNaN = __builtin_nan("");
+
+// Two IEEE f64 divisions qa = a1 / b1, qb = a2 / b2 with the compiler's own
+// instruction sequence (v_div_scale, v_rcp, two Newton steps, v_div_fmas,
+// v_div_fixup: correctly rounded for every input), interleaved by hand.  The
+// compiler emits each division as a dependent chain that waits on the
+// v_rcp result and on VCC before v_div_fmas (an s_nop each, 2 of 13 issue
+// slots); two chains fill each other's waits.  VCC carries the numerator's
+// scale flag from v_div_scale to v_div_fmas, so the two flag windows are
+// sequential: A's flag is written early (it only needs the inputs) and read
+// 5 instructions later; B's is written after A's v_div_fmas and read after
+// 3 instructions + 1 wait state (4 are required).
+#ifndef RWRT_DIV2_ASM
+#define RWRT_DIV2_ASM 1
+#endif
+__device__ __forceinline__ void div2(double a1, double b1, double a2, double b2, double& qa,
+                                     double& qb) {
+#if RWRT_DIV2_ASM
+  double dA, dB, rA, rB, eA, eB, nA, nB;
+  asm(
+      "v_div_scale_f64 %[dA], vcc, %[bA], %[bA], %[aA]\n\t"
+      "v_div_scale_f64 %[dB], vcc, %[bB], %[bB], %[aB]\n\t"
+      "v_rcp_f64 %[rA], %[dA]\n\t"
+      "v_rcp_f64 %[rB], %[dB]\n\t"
+      "v_fma_f64 %[eA], -%[dA], %[rA], 1.0\n\t"
+      "v_fma_f64 %[eB], -%[dB], %[rB], 1.0\n\t"
+      "v_fma_f64 %[rA], %[rA], %[eA], %[rA]\n\t"
+      "v_fma_f64 %[rB], %[rB], %[eB], %[rB]\n\t"
+      "v_fma_f64 %[eA], -%[dA], %[rA], 1.0\n\t"
+      "v_div_scale_f64 %[nA], vcc, %[aA], %[bA], %[aA]\n\t"
+      "v_fma_f64 %[eB], -%[dB], %[rB], 1.0\n\t"
+      "v_fma_f64 %[rA], %[rA], %[eA], %[rA]\n\t"
+      "v_fma_f64 %[rB], %[rB], %[eB], %[rB]\n\t"
+      "v_mul_f64 %[qA], %[nA], %[rA]\n\t"
+      "v_fma_f64 %[eA], -%[dA], %[qA], %[nA]\n\t"
+      "v_div_fmas_f64 %[qA], %[eA], %[rA], %[qA]\n\t"
+      "v_div_scale_f64 %[nB], vcc, %[aB], %[bB], %[aB]\n\t"
+      "v_mul_f64 %[qB], %[nB], %[rB]\n\t"
+      "v_fma_f64 %[eB], -%[dB], %[qB], %[nB]\n\t"
+      "v_div_fixup_f64 %[qA], %[qA], %[bA], %[aA]\n\t"
+      "s_nop 0\n\t"
+      "v_div_fmas_f64 %[qB], %[eB], %[rB], %[qB]\n\t"
+      "v_div_fixup_f64 %[qB], %[qB], %[bB], %[aB]"
+      : [qA] "=&v"(qa), [qB] "=&v"(qb), [dA] "=&v"(dA), [dB] "=&v"(dB), [rA] "=&v"(rA),
+        [rB] "=&v"(rB), [eA] "=&v"(eA), [eB] "=&v"(eB), [nA] "=&v"(nA), [nB] "=&v"(nB)
+      : [aA] "v"(a1), [bA] "v"(b1), [aB] "v"(a2), [bB] "v"(b2)
+      : "vcc");
+#else
+  qa = a1 / b1;
+  qb = a2 / b2;
+#endif
+}
 #if RWRT_DIAG_NODIV   // timing-only diagnostic build: approximate quotients in the RHS
 #define RDIV(a, b) ((a) * __builtin_amdgcn_rcp(b))
 #else
@@ -235,8 +286,8 @@ struct Corners {
 __device__ __forceinline__ Corners corners(const Field& F, double lon, double lat) {
   // lon arrives already reduced once (bs.py:519); interpolation.py:80 reduces again.
   const double lons = py_mod_2pi_again(lon);
-  const double x = div_uniform(lons - F.lon0, F.dlon);
-  const double y = div_uniform(lat - F.lat0, F.dlat);
+  double x, y;
+  div2(lons - F.lon0, F.dlon, lat - F.lat0, F.dlat, x, y);
   const int ix = floor_i32(x), iy = floor_i32(y);
   const int x0 = clip(ix, F.W - 1), x1 = clip(inc_i32(ix), F.W - 1);
   const int y0 = clip(iy, F.H - 1), y1 = clip(inc_i32(iy), F.H - 1);
@@ -481,8 +532,8 @@ struct VaryingBG {
   __device__ __forceinline__ void cell(double lon, double lat, unsigned o[4], double w[4],
                                        unsigned& key_x, unsigned& key_y) const {
     const double lons = py_mod_2pi_again(py_mod_2pi(lon));
-    const double x = div_uniform(lons - lon0, dlon);
-    const double y = div_uniform(lat - lat0, dlat);
+    double x, y;
+    div2(lons - lon0, dlon, lat - lat0, dlat, x, y);
     const int ix = floor_i32(x), iy = floor_i32(y);
     const int x0 = clip(ix, W - 1), x1 = clip(inc_i32(ix), W - 1);
     const int y0 = clip(iy, H - 1), y1 = clip(inc_i32(iy), H - 1);
@@ -840,11 +891,9 @@ __device__ __forceinline__ void mercator12_masked(const double g[11], const Merc
 __device__ __forceinline__ void mercator12(const double g[11], const Merc& M, double t, double o[12]) {
   const double cp = M.c;
   const double fu = g[F_U], fv = g[F_V];
-  o[0] = RDIV(fu, cp);
-  o[1] = RDIV(fv, cp);
-  o[2] = RDIV(g[F_UX], cp);
+  div2(fu, cp, fv, cp, o[0], o[1]);
+  div2(g[F_UX], cp, g[F_VX], cp, o[2], o[4]);
   o[3] = g[F_UY] + t * fu;
-  o[4] = RDIV(g[F_VX], cp);
   o[5] = g[F_VY] + t * fv;
   o[6] = g[F_QX];
   o[7] = g[F_QY] * cp;
@@ -866,8 +915,11 @@ __device__ __forceinline__ void ugvg(double fu, double fv, double fqx, double fq
   const double kap1 = 1.0 + kap2;
   const double KK = (k * k) * kap1;
   const double denom = KK * kap1;
-  ug = fu + RDIV(((1.0 - kap2) * fqy) - ((2.0 * kap) * fqx), denom);
-  vg = fv + RDIV(((2.0 * kap) * fqy) + ((1.0 - kap2) * fqx), denom);
+  double qu, qv;
+  div2(((1.0 - kap2) * fqy) - ((2.0 * kap) * fqx), denom,
+       ((2.0 * kap) * fqy) + ((1.0 - kap2) * fqx), denom, qu, qv);
+  ug = fu + qu;
+  vg = fv + qv;
 }
 
 // ---------------------------------------------------------------------------
@@ -930,16 +982,17 @@ __device__ __forceinline__ void ray_rhs(const BG& B, double t, const double* y, 
   const double kap2 = kap * kap;
   const double kap1 = 1.0 + kap * kap;
   const double kk = (kx * kx) * kap1;
-  const double dzwn = (-kx) * ((fmux + kap * fmvx) + RDIV(kap * fmqxx - fmqyx, kk));
-  const double dmwn = (-kx) * ((fmuy + kap * fmvy) + RDIV(kap * fmqxy - fmqyy, kk));
-  const double damp1 = RDIV(2.0 * ((fmux + fmvy) + kap * (fmvx + fmuy)), kap1);
-  const double damp2 = RDIV(2.0 * (kap * (fmqxx - fmqyy) + (kap2 - 1.0) * fmqxy), kk * kap1);
+  double qk, ql;
+  div2(kap * fmqxx - fmqyx, kk, kap * fmqxy - fmqyy, kk, qk, ql);
+  const double dzwn = (-kx) * ((fmux + kap * fmvx) + qk);
+  const double dmwn = (-kx) * ((fmuy + kap * fmvy) + ql);
+  double damp1, damp2;
+  div2(2.0 * ((fmux + fmvy) + kap * (fmvx + fmuy)), kap1,
+       2.0 * (kap * (fmqxx - fmqyy) + (kap2 - 1.0) * fmqxy), kk * kap1, damp1, damp2);
   const double damp3 = (-2.0 * s) * fmv;
   const double damp = (damp1 + damp2) + damp3;
-  dy[0] = div_rearth(ug);
-  dy[1] = div_rearth(vg * c);
-  dy[2] = div_rearth(dzwn);
-  dy[3] = div_rearth(dmwn);
+  div2(ug, kREarth, vg * c, kREarth, dy[0], dy[1]);     // x / R, x / R
+  div2(dzwn, kREarth, dmwn, kREarth, dy[2], dy[3]);
   dy[4] = div_rearth(damp * amp);
   if (aux) {
     aux[0] = ug;
@@ -1649,6 +1702,8 @@ __global__ void math_kernel(int kind, int64_t n, const double* __restrict__ x,
     case 20: r = rm_pow(a, b); break;
     case 21: r = rwrt_math::rm_exp(a); break;
     case 22: r = recip2(a); break;
+    case 23: { double q1, q2; div2(a, b, b, a, q1, q2); r = q1; } break;
+    case 24: { double q1, q2; div2(b, a, a, b, q1, q2); r = q2; } break;
     default: r = fmod_pos(a, b); break;
   }
   out[i] = r;
@@ -2348,7 +2403,7 @@ rwrt_status rwrt_kat_rk45(int32_t kind, int64_t ncol, const double* d_y0, int32_
 
 rwrt_status rwrt_selftest_math(int32_t kind, int64_t n, const double* d_x, const double* d_y,
                                double* d_out, void* stream) {
-  if (n < 0 || kind < 0 || kind > 22 || (n > 0 && (!d_x || !d_out)))
+  if (n < 0 || kind < 0 || kind > 24 || (n > 0 && (!d_x || !d_out)))
     return fail(RWRT_ERR_ARG, "bad selftest arguments%s");
   if (n == 0) return RWRT_OK;
   hipLaunchKernelGGL(math_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, kind,

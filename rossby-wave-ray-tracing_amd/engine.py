@@ -427,7 +427,8 @@ MATH_KINDS = {"sin": 0, "cos": 1, "tan": 2, "pow": 3, "atan2": 4, "mod": 5, "sqr
               "div": 7, "floor": 8, "sincos_sin": 9, "sincos_cos": 10, "div_rearth": 11,
               "fmod": 12, "mod2pi": 13, "mod2pi_twice": 14, "div_hw": 15, "floor_i32": 16,
               "sct_sin": 17, "sct_cos": 18, "sct_tan": 19, "rm_pow": 20, "rm_exp": 21,
-              "recip2": 22}
+              "recip2": 22, "div2_first": 23,
+              "div2_second": 24}
 
 
 def selftest_math(name, x, y=None, device="cuda"):

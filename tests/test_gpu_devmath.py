@@ -150,3 +150,26 @@ def test_time_varying_c2_bitwise_with_device_math(fp32):
     g = np.transpose(hist[:, :, :7], (2, 1, 0))
     assert same(g, ref[:, 1:]), int((~((g == ref[:, 1:]) | (np.isnan(g) & np.isnan(ref[:, 1:])))).sum())
     assert np.array_equal(res.nacc.cpu().numpy(), nacc)
+
+
+def test_interleaved_division_pair_is_ieee():
+    """div2 (two IEEE divisions interleaved in inline asm) == a / b bit for bit,
+    as either quotient of the pair, on random, extreme and special operands."""
+    from engine import selftest_math as dev
+    rng = np.random.default_rng(5)
+    n = 1 << 21
+    a = rng.standard_normal(n) * 10.0 ** rng.uniform(-308, 308, n)
+    b = rng.standard_normal(n) * 10.0 ** rng.uniform(-308, 308, n)
+    phys_a = rng.standard_normal(n) * 10.0 ** rng.uniform(-15, 8, n)
+    phys_b = rng.uniform(0.01, 1.0, n) * rng.choice([-1, 1], n)
+    sp = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 5e-324, -5e-324, 2.2250738585072014e-308,
+                   1.7976931348623157e308, -1.7976931348623157e308, 1.0, -1.0, 6.3712e6, 3.0, 0.1])
+    ea, eb = np.meshgrid(sp, sp)
+    a = np.concatenate([a, phys_a, ea.ravel(), rng.standard_normal(1000) * 1e-310,
+                        np.full(1000, 1e308)])
+    b = np.concatenate([b, phys_b, eb.ravel(), rng.standard_normal(1000) * 1e300,
+                        rng.standard_normal(1000) * 1e-10])
+    with np.errstate(all="ignore"):
+        want = a / b
+    assert same(dev("div2_first", a, b), want)
+    assert same(dev("div2_second", a, b), want)
