@@ -48,7 +48,9 @@ constexpr double kRInv = 1.0 / 6.3712e6;   // RN(1 / R)
 #define RWRT_DIV_REARTH_IEEE 1
 #endif
 __device__ __forceinline__ double div_rearth(double x) {
-#if RWRT_DIV_REARTH_IEEE
+#if RWRT_DIAG_NODIV
+  return x * kRInv;
+#elif RWRT_DIV_REARTH_IEEE
   return x / kREarth;
 #endif
   const double ax = fabs(x);
@@ -78,7 +80,10 @@ constexpr double kNaN = __builtin_nan("");
 #endif
 __device__ __forceinline__ void div2(double a1, double b1, double a2, double b2, double& qa,
                                      double& qb) {
-#if RWRT_DIV2_ASM
+#if RWRT_DIAG_NODIV   // timing-only diagnostic build: approximate quotients
+  qa = a1 * __builtin_amdgcn_rcp(b1);
+  qb = a2 * __builtin_amdgcn_rcp(b2);
+#elif RWRT_DIV2_ASM
   double dA, dB, rA, rB, eA, eB, nA, nB;
   asm(
       "v_div_scale_f64 %[dA], vcc, %[bA], %[bA], %[aA]\n\t"
