@@ -154,7 +154,7 @@ def main():
     ap.add_argument("--days", type=float, default=90.0, help="integration horizon per step")
     ap.add_argument("--chunk", type=int, default=0, help="output rows per kernel launch")
     ap.add_argument("--cpu-rays", type=int, default=16384)
-    ap.add_argument("--cpu-days", type=float, default=4.0)
+    ap.add_argument("--cpu-days", type=float, default=12.0)   # ~10 s of 1-core oracle work
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-procs", type=int, default=16,
                     help="processes of the multi-core CPU baseline (1: skip it)")
@@ -298,6 +298,10 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK,
                          "traffic": traffic["traffic_bytes_per_launch"] if traffic else None,
+                         "traffic_rate_GBps": (traffic["traffic_bytes_per_launch"] / avg_launch_s / 1e9
+                                               if traffic else None),
+                         "algorithmic_note": ("algorithmic bytes per SURVEY.md 8(d), most served from the "
+                                              "LDS lookup cache and L2; traffic = real HBM bytes (PMC)"),
                          "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
                          "traffic_source": tsrc,
                          "algorithmic_bytes_per_launch": per_launch_steps * BYTES_PER_STEP,
@@ -325,7 +329,7 @@ def main():
                           sink=lambda a, b, o: rows.__setitem__(a, o[:, :, :7].cpu().numpy()))
             gpu = np.concatenate([rows[k] for k in sorted(rows)], axis=1)   # rows 1..cnt-1
             parity = []
-            for row in sorted({min(12, cnt - 1), cnt - 1}):
+            for row in sorted({min(12, cnt - 1), min(48, cnt - 1), cnt - 1}):
                 g, c = gpu[:, row - 1, :2], hist[:2, row].T
                 ok = ~np.isnan(g).any(1) & ~np.isnan(c).any(1)
                 d = np.max(np.abs(g[ok] - c[ok]), axis=1) if ok.any() else np.zeros(1)
@@ -447,6 +451,10 @@ def main_c5(args, dist, rank, world, dev):
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK,
                          "traffic": traffic["traffic_bytes_per_launch"] if traffic else None,
+                         "traffic_rate_GBps": (traffic["traffic_bytes_per_launch"] / avg_launch_s / 1e9
+                                               if traffic else None),
+                         "algorithmic_note": ("algorithmic bytes per SURVEY.md 8(d), most served from the "
+                                              "LDS lookup cache and L2; traffic = real HBM bytes (PMC)"),
                          "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
                          "traffic_source": tsrc,
                          "algorithmic_bytes_per_launch": per_launch_steps * bps,

@@ -65,6 +65,28 @@ __device__ __forceinline__ double div_rearth(double x) {
 }
 constexpr double kNaN = __builtin_nan("");
 
+// Output rows are written once and never read back by the kernels: stores
+// marked non-temporal stream past the L2 instead of evicting the basic state
+// and solver state the ray loop re-reads.
+#ifndef RWRT_NT_ROWS
+#define RWRT_NT_ROWS 0
+#endif
+#ifndef RWRT_NT_FILL
+#define RWRT_NT_FILL 1
+#endif
+typedef double v2f64 __attribute__((ext_vector_type(2)));
+template <bool NT>
+__device__ __forceinline__ void store_row16(double2* o, double2 v) {
+  if (NT) {
+    v2f64 w;
+    w.x = v.x;
+    w.y = v.y;
+    __builtin_nontemporal_store(w, reinterpret_cast<v2f64*>(o));
+  } else {
+    *o = v;
+  }
+}
+
 // Two IEEE f64 divisions qa = a1 / b1, qb = a2 / b2 with the compiler's own
 // instruction sequence (v_div_scale, v_rcp, two Newton steps, v_div_fmas,
 // v_div_fixup: correctly rounded for every input), interleaved by hand.  The
@@ -1509,6 +1531,7 @@ struct RunArgs {
   int64_t n_heavy;      // order[0, n_heavy) = heavy queue, the rest = light queue
   int32_t heavy_blocks; // blocks [0, heavy_blocks) serve the heavy queue first
   double cut_a;         // haversine argument certainly below cut_off (cal_dis_below)
+  const uint8_t* frozen;  // rays frozen at the launch start (NULL: none skipped), see frozen_fill_kernel
 };
 
 // Haversine threshold: d = 2 atan2(sqrt(a), sqrt(1 - a)) increases with a, so
@@ -1533,6 +1556,12 @@ inline double haversine_cut(double cut_off) {
 // while the normal-priority waves fill every stall.
 #ifndef RWRT_WAVES_PER_SIMD
 #define RWRT_WAVES_PER_SIMD 1
+#endif
+#ifndef RWRT_RUN_PRIO
+#define RWRT_RUN_PRIO 1
+#endif
+#ifndef RWRT_DIAG_NOFROZENFILL   // timing-only diagnostic build: frozen rays write one row
+#define RWRT_DIAG_NOFROZENFILL 0
 #endif
 #ifndef RWRT_K_IN_LDS
 #define RWRT_K_IN_LDS 1   // stages in LDS: frees 60 VGPRs (in registers they spill to scratch)
@@ -1563,7 +1592,13 @@ __global__ void __launch_bounds__(256, RWRT_WAVES_PER_SIMD) rk45_run_kernel(RunA
   double prev_lon = 0.0, prev_lat = 0.0, cos_prev = 0.0;
   const bool heavy = (int)blockIdx.x < a.heavy_blocks;
   bool heavy_left = heavy && a.n_heavy > 0;
-  if (heavy) __builtin_amdgcn_s_setprio(3);
+  if (heavy) {
+    __builtin_amdgcn_s_setprio(3);
+  } else if (RWRT_RUN_PRIO) {
+    // above frozen_fill_kernel's waves (priority 0) sharing the SIMD: the
+    // fill takes the issue cycles the ray loop leaves idle
+    __builtin_amdgcn_s_setprio(1);
+  }
   for (;;) {
     if (ray < 0) {
       int64_t w = -1;
@@ -1579,6 +1614,10 @@ __global__ void __launch_bounds__(256, RWRT_WAVES_PER_SIMD) rk45_run_kernel(RunA
         if (w >= a.nray) break;
       }
       ray = a.order ? a.order[w] : w;
+      if (a.frozen && a.frozen[ray]) {   // its rows come from frozen_fill_kernel
+        ray = -1;
+        continue;
+      }
 #pragma unroll
       for (int v = 0; v < 5; ++v) {
         L.y[v] = a.state[v * a.nray + ray];
@@ -1641,12 +1680,12 @@ __global__ void __launch_bounds__(256, RWRT_WAVES_PER_SIMD) rk45_run_kernel(RunA
     const int last = (st == Lane<RayProblem, KStore>::kFrozen) ? a.it_end : it + 1;
     {
       double2* o = reinterpret_cast<double2*>(a.out + ((size_t)ray * nrows + (it - a.it_begin)) * RWRT_NOUT);
-      o[0] = r0;
-      o[1] = r1;
-      o[2] = r2;
-      o[3] = r3;
+      store_row16<RWRT_NT_ROWS>(o + 0, r0);
+      store_row16<RWRT_NT_ROWS>(o + 1, r1);
+      store_row16<RWRT_NT_ROWS>(o + 2, r2);
+      store_row16<RWRT_NT_ROWS>(o + 3, r3);
     }
-    if (last > it + 1) {
+    if (!RWRT_DIAG_NOFROZENFILL && last > it + 1) {
       asm volatile("");   // frozen: the remaining rows of the chunk (rare branch)
       for (int k = it + 1; k < last; ++k) {
         double2* o = reinterpret_cast<double2*>(a.out + ((size_t)ray * nrows + (k - a.it_begin)) * RWRT_NOUT);
@@ -1675,6 +1714,103 @@ __global__ void __launch_bounds__(256, RWRT_WAVES_PER_SIMD) rk45_run_kernel(RunA
       a.nanrow[ray] = nanrow;
       ray = -1;
     }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Rays frozen at the launch start (NaN mean: dead root slots, rays masked in
+// an earlier chunk) never change again (rkf45.py:400-403); rk45_run_kernel's
+// lanes would each spend one attempt-sized detour writing their constant
+// rows (up to ~1000 x 64 B per ray, 70 % of C3's output bytes, with the other
+// lanes of the wave idle).  launch_run instead flags them (frozen_flag_kernel),
+// the run kernel skips them, and frozen_fill_kernel -- on a side stream,
+// overlapping the run kernel in the registers and LDS it leaves free --
+// computes each one's row exactly as the run kernel's frozen path does (the
+// same masks and group velocity) and writes the chunk's rows with coalesced
+// 16-B stores.
+// ---------------------------------------------------------------------------
+__global__ void frozen_flag_kernel(const double* __restrict__ state, int64_t nray,
+                                   uint8_t* __restrict__ frozen) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nray;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    double sum = state[i];
+#pragma unroll
+    for (int v = 1; v < 5; ++v) sum = sum + state[v * nray + i];
+    frozen[i] = isnan(sum / 5.0) ? 1 : 0;   // Lane::iterate's NaN-mean test
+  }
+}
+
+// At most 128 VGPRs: a fill wave must fit beside the run kernel's wave in a
+// SIMD's register file (256 VGPRs + its AGPRs of 512), and its 8.7 KB of LDS
+// beside the run kernel's 146 KB, or the fill would wait for the run to end.
+constexpr int kFillThreads = 128;
+#ifndef RWRT_FILL_THROTTLE
+#define RWRT_FILL_THROTTLE 256
+#endif
+template <class BG>
+__global__ void __launch_bounds__(kFillThreads) __attribute__((amdgpu_num_vgpr(128)))
+frozen_fill_kernel(RunArgs<BG> a) {
+  __shared__ double2 rowbuf[kFillThreads][4];
+  __shared__ int list[kFillThreads];
+  __shared__ int cnt;
+  const int64_t nrows = a.it_end - a.it_begin;
+  const int64_t base = blockIdx.x * (int64_t)kFillThreads;
+  if (threadIdx.x == 0) cnt = 0;
+  __syncthreads();
+  const int64_t ray = base + threadIdx.x;
+  if (ray < a.nray && a.frozen[ray]) {
+    // rk45_run_kernel's fetch + kFrozen iteration + post-processing, verbatim
+    double y[5];
+#pragma unroll
+    for (int v = 0; v < 5; ++v) y[v] = a.state[v * a.nray + ray];
+    const int64_t nacc = a.count[2 * ray];
+    int32_t nanrow = a.nanrow[ray];
+    const int32_t it = a.it_begin;
+    const double prev_lon = y[0], prev_lat = y[1];
+    const double cos_prev = cos(prev_lat);
+    const double tb = a.tbound[it];
+    double ug, vg, cos_c = kNaN;
+    bool masked = fabs(y[1]) >= kHalfPi;
+    if (!masked) {
+      cos_c = cos_small(y[1]);
+      masked = cal_dis_reaches(y[0], y[1], prev_lon, prev_lat, cos_c, cos_prev, a.cut_off, a.cut_a);
+    }
+    if (masked) {
+#pragma unroll
+      for (int v = 0; v < 5; ++v) y[v] = kNaN;
+      ug = vg = kNaN;
+    } else {
+      ugvg_at(a.B, tb, y[0], y[1], y[2], y[3], ug, vg);
+    }
+    const double2 r0 = make_double2(y[0], y[1]), r1 = make_double2(y[2], y[3]);
+    const double2 r2 = make_double2(y[4], ug), r3 = make_double2(vg, (double)nacc);
+    rowbuf[threadIdx.x][0] = r0;
+    rowbuf[threadIdx.x][1] = r1;
+    rowbuf[threadIdx.x][2] = r2;
+    rowbuf[threadIdx.x][3] = r3;
+    if (nanrow == a.nt && isnan(y[0])) nanrow = it;   // wr.py:853-855
+#pragma unroll
+    for (int v = 0; v < 5; ++v) a.state[v * a.nray + ray] = y[v];
+    a.state[10 * a.nray + ray] = a.tbound[a.it_end - 1];
+    a.nanrow[ray] = nanrow;
+    list[atomicAdd(&cnt, 1)] = threadIdx.x;
+  }
+  __syncthreads();
+  // every row of the chunk for each frozen ray of the tile: the block writes
+  // one ray's rows at a time, 16 B per thread, contiguous (a ray's rows are)
+  const int n = cnt;
+  const int64_t nq = nrows * 4;
+  for (int k = 0; k < n; ++k) {
+    const int j = list[k];
+    double2* o = reinterpret_cast<double2*>(a.out + (size_t)(base + j) * nrows * RWRT_NOUT);
+    const double2 v = rowbuf[j][threadIdx.x & 3];
+    for (int64_t q = threadIdx.x; q < nq; q += kFillThreads) store_row16<RWRT_NT_FILL>(o + q, v);
+#if RWRT_FILL_THROTTLE
+    // pace the stores (~4 us per full RWRT_FILL_THROTTLE rows; none for short
+    // chunks): a full-rate fill floods the memory queues the run kernel's
+    // lookups wait in
+    for (int64_t z = RWRT_FILL_THROTTLE; z <= nrows; z += RWRT_FILL_THROTTLE) __builtin_amdgcn_s_sleep(127);
+#endif
   }
 }
 
@@ -2028,6 +2164,44 @@ rwrt_status launch_init(const BG& B, int64_t nray, const double* d_y0, const rwr
   return check_launch("rk45_init_kernel");
 }
 
+#ifndef RWRT_FROZEN_FILL
+#define RWRT_FROZEN_FILL 1
+#endif
+// Per-device scratch of launch_run: the frozen flags (one byte per ray, grown
+// on demand), the side stream of frozen_fill_kernel and its two events.
+struct FillScratch {
+  uint8_t* flags = nullptr;
+  size_t cap = 0;
+  hipStream_t side = nullptr;
+  hipEvent_t flagged = nullptr, filled = nullptr;
+};
+FillScratch* fill_scratch(int64_t nray) {
+  static FillScratch cache[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  FillScratch& f = cache[dev];
+  if (!f.side) {
+    if (hipStreamCreateWithFlags(&f.side, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&f.flagged, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&f.filled, hipEventDisableTiming) != hipSuccess) {
+      f.side = nullptr;
+      return nullptr;
+    }
+  }
+  if ((size_t)nray > f.cap) {
+    if (f.flags) {
+      // earlier launches may still read the old flags
+      if (hipDeviceSynchronize() != hipSuccess || hipFree(f.flags) != hipSuccess) return nullptr;
+      f.flags = nullptr;
+      f.cap = 0;
+    }
+    const size_t cap = ((size_t)nray + 4095) & ~(size_t)4095;
+    if (hipMalloc(reinterpret_cast<void**>(&f.flags), cap) != hipSuccess) return nullptr;
+    f.cap = cap;
+  }
+  return &f;
+}
+
 template <class BG>
 rwrt_status launch_run(const BG& B, int64_t nray, const rwrt_params* p, const double* d_tbound,
                        int32_t it_begin, int32_t it_end, const int64_t* d_order, int64_t n_heavy,
@@ -2053,9 +2227,32 @@ rwrt_status launch_run(const BG& B, int64_t nray, const rwrt_params* p, const do
   const int heavy_blocks = (d_order && n_heavy > 0 && blocks >= 2 * (int64_t)ncu) ? ncu : 0;
   RunArgs<BG> a{B, nray, p->rtol, p->atol, p->min_step, p->cut_off, p->nt, it_begin, it_end,
                 d_tbound, d_order, d_state, d_count, d_nanrow, d_out, d_work,
-                heavy_blocks ? n_heavy : 0, heavy_blocks, haversine_cut(p->cut_off)};
+                heavy_blocks ? n_heavy : 0, heavy_blocks, haversine_cut(p->cut_off), nullptr};
+#if RWRT_FROZEN_FILL
+  // frozen rays: flagged on `stream`, filled on the side stream while the run
+  // kernel (which skips them) integrates the rest; `stream` then waits for
+  // the fill, so the call stays one stream-ordered operation for the caller
+  FillScratch* fs = fill_scratch(nray);
+  if (!fs) return fail(RWRT_ERR_HIP, "frozen-ray scratch allocation failed%s");
+  a.frozen = fs->flags;
+  hipLaunchKernelGGL(frozen_flag_kernel, dim3(grid_for(nray, 256)), dim3(256), 0, (hipStream_t)stream,
+                     d_state, nray, fs->flags);
+  if (rwrt_status s = check_launch("frozen_flag_kernel")) return s;
+  if (hipEventRecord(fs->flagged, (hipStream_t)stream) != hipSuccess ||
+      hipStreamWaitEvent(fs->side, fs->flagged, 0) != hipSuccess)
+    return check_launch("hipEventRecord(frozen flags)");
+#endif
   hipLaunchKernelGGL(rk45_run_kernel<BG>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
-  return check_launch("rk45_run_kernel");
+  if (rwrt_status s = check_launch("rk45_run_kernel")) return s;
+#if RWRT_FROZEN_FILL
+  hipLaunchKernelGGL(frozen_fill_kernel<BG>, dim3((unsigned)((nray + kFillThreads - 1) / kFillThreads)),
+                     dim3(kFillThreads), 0, fs->side, a);
+  if (rwrt_status s = check_launch("frozen_fill_kernel")) return s;
+  if (hipEventRecord(fs->filled, fs->side) != hipSuccess ||
+      hipStreamWaitEvent((hipStream_t)stream, fs->filled, 0) != hipSuccess)
+    return check_launch("hipEventRecord(frozen fill)");
+#endif
+  return RWRT_OK;
 }
 
 // a time-varying background from the ABI description

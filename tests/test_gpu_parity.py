@@ -292,6 +292,20 @@ def test_time_chunking_is_bitwise_invisible():
     assert torch.equal(r1.nacc, r2.nacc)
 
 
+def test_frozen_rays_filled_like_the_run_kernel():
+    """Rays frozen at a launch start (dead slots, rays masked in an earlier
+    chunk) are written by frozen_fill_kernel on a side stream; chunked runs,
+    where many rays enter later chunks frozen, equal one launch bit for bit
+    (rows, accepted/rejected counts, first-NaN rows, the early-exit row)."""
+    h1, r1 = run_c2("nonzonal", 241)
+    h2, r2 = run_c2("nonzonal", 241, chunk=40)
+    frozen_later = np.isnan(h1[:, 40, 0]) & ~np.isnan(h1[:, 0, 3])
+    assert frozen_later.sum() > 0            # rays masked in the first chunk exist
+    assert np.array_equal(h1, h2, equal_nan=True)
+    assert torch.equal(r1.nacc, r2.nacc) and torch.equal(r1.nrej, r2.nrej)
+    assert torch.equal(r1.nanrow, r2.nanrow) and r1.break_row == r2.break_row
+
+
 def test_sharding_is_bitwise_invisible():
     """Rays are independent: any split into shards reproduces the unsharded run."""
     g = golden("init_C2_nonzonal.npz")

@@ -1,4 +1,6 @@
-"""Per-launch HBM traffic of rk45_run_kernel from two rocprofv3 PMC passes.
+"""Per-launch HBM traffic of one rwrt_rk45_run call (rk45_run_kernel plus the
+frozen-ray flag and fill kernels it launches beside it) from two rocprofv3 PMC
+passes.
 
     python tools/pmc_traffic.py <fetch_dir> <write_dir> <bench_json_log> <out.json>
 
@@ -13,12 +15,18 @@ import json
 import sys
 
 
+KERNELS = ("rk45_run_kernel", "frozen_fill_kernel", "frozen_flag_kernel")
+
+
 def per_launch(d, counter):
-    vals = []
+    """Bytes per rwrt_rk45_run call: the calls' kernels summed, divided over
+    the rk45_run_kernel dispatches (one per call)."""
+    total, launches = 0.0, 0
     for r in csv.DictReader(open(f"{d}/run_counter_collection.csv")):
-        if "rk45_run_kernel" in r["Kernel_Name"] and r["Counter_Name"] == counter:
-            vals.append(float(r["Counter_Value"]) * 1024.0)
-    return vals
+        if r["Counter_Name"] == counter and any(k in r["Kernel_Name"] for k in KERNELS):
+            total += float(r["Counter_Value"]) * 1024.0
+            launches += "rk45_run_kernel" in r["Kernel_Name"]
+    return [total / max(launches, 1)] * launches
 
 
 def main():
@@ -33,7 +41,7 @@ def main():
     fb, wb = sum(f[:n]) / n, sum(w[:n]) / n
     steps_per_launch = bench["ray_steps_per_step"] / (bench["roofline"]["launches"] / bench["steps"])
     res = {"workload": bench["config"]["workload"], "launch_rows": bench["config"].get("launch_rows"),
-           "kernel": "rk45_run_kernel", "launches": n,
+           "kernel": "rk45_run_kernel", "kernels_summed": list(KERNELS), "launches": n,
            "fetch_bytes_per_launch_x2": 2 * fb, "write_bytes_per_launch": wb,
            "traffic_bytes_per_launch": 2 * fb + wb,
            "algorithmic_bytes_per_launch": steps_per_launch * bench["roofline"]["bytes_per_ray_step"],
