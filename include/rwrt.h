@@ -156,7 +156,12 @@ rwrt_status rwrt_rk45_init(const rwrt_grid* g, const double* d_packed,
  * ray j is d_out[(j*(it_end-it_begin) + r)*8 + {lon,lat,k,l,amp,ug,vg,nacc}].
  * d_state / d_count / d_nanrow carry the per-ray solver state across calls
  * (time chunking).  d_work: >= 2 int32 of scratch (queue heads), reset by
- * this call on `stream`.  Results do not depend on the order or n_heavy. */
+ * this call on `stream`.  Results do not depend on the order or n_heavy.
+ * Rays frozen at the call's start (NaN in their state) are flagged in
+ * library-owned scratch (1 byte per ray per device, grown on demand) and
+ * their rows written by a kernel on a library side stream; `stream` waits
+ * for it, so the call remains one stream-ordered operation (also for
+ * rwrt_rk45_run_tv). */
 rwrt_status rwrt_rk45_run(const rwrt_grid* g, const double* d_packed,
                           int64_t nray, const rwrt_params* p,
                           const double* d_tbound, int32_t it_begin,
