@@ -2153,7 +2153,8 @@ rwrt_status launch_init(const BG& B, int64_t nray, const double* d_y0, const rwr
                         int64_t* d_summary, void* stream) {
   if (!p) return fail(RWRT_ERR_ARG, "params is NULL%s");
   if (nray < 0 || nray > 0x7fffffffLL) return fail(RWRT_ERR_ARG, "nray out of range%s");
-  if (!d_y0 || !d_state || !d_count || !d_nanrow || !d_live || !d_summary)
+  // per-ray buffers of an empty batch may be NULL (empty tensors)
+  if (!d_summary || (nray > 0 && (!d_y0 || !d_state || !d_count || !d_nanrow || !d_live)))
     return fail(RWRT_ERR_ARG, "NULL buffer to rwrt_rk45_init%s");
   if (hipMemsetAsync(d_summary, 0, 2 * sizeof(int64_t), (hipStream_t)stream) != hipSuccess)
     return check_launch("hipMemsetAsync(summary)");
@@ -2211,7 +2212,7 @@ rwrt_status launch_run(const BG& B, int64_t nray, const rwrt_params* p, const do
   if (nray < 0 || nray > 0x7fffffffLL) return fail(RWRT_ERR_ARG, "nray out of range%s");
   if (it_begin < 1 || it_end > p->nt || it_begin >= it_end)
     return fail(RWRT_ERR_ARG, "need 1 <= it_begin < it_end <= nt%s");
-  if (!d_tbound || !d_state || !d_count || !d_nanrow || !d_out || !d_work)
+  if (!d_tbound || !d_work || (nray > 0 && (!d_state || !d_count || !d_nanrow || !d_out)))
     return fail(RWRT_ERR_ARG, "NULL buffer to rwrt_rk45_run%s");
   if (reinterpret_cast<uintptr_t>(d_out) % 16 != 0)
     return fail(RWRT_ERR_ARG, "output rows must be 16-byte aligned%s");
@@ -2572,7 +2573,7 @@ rwrt_status rwrt_rk4_run(const rwrt_grid* g, const double* d_packed, int64_t nra
   if (it_begin < 1 || it_end > p->nt || it_begin >= it_end)
     return fail(RWRT_ERR_ARG, "need 1 <= it_begin < it_end <= nt%s");
   if (!(p->tstep > 0.0)) return fail(RWRT_ERR_ARG, "tstep must be positive%s");
-  if (!d_state || !d_count || !d_nanrow || !d_out || !d_work)
+  if (!d_work || (nray > 0 && (!d_state || !d_count || !d_nanrow || !d_out)))
     return fail(RWRT_ERR_ARG, "NULL buffer to rwrt_rk4_run%s");
   if (reinterpret_cast<uintptr_t>(d_out) % 16 != 0)
     return fail(RWRT_ERR_ARG, "output rows must be 16-byte aligned%s");

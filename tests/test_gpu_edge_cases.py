@@ -1,0 +1,120 @@
+"""Edge cases of the ray loop on the GPU, bitwise against the oracle on the
+device's own sin/cos/tan/pow (``rwrt_oracle.device_math()``).
+
+* empty batches (nray = 0) launch nothing and return empty results;
+* ragged batch sizes around the block and fill-tile sizes (1, 127, 129, 300
+  rays; 256-lane blocks, 128-ray fill tiles) with live and dead slots mixed,
+  integrated in 7-row chunks so that rays also enter later chunks frozen;
+* batches where every ray is frozen from the start (dead root slots: finite
+  source position, NaN wavenumber) -- only frozen_fill_kernel writes rows;
+* an all-NaN batch: the reference's early exit (wr.py:853-855) at row 1.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+import synthetic as S
+
+pytestmark = pytest.mark.gpu
+NT = 25
+
+
+def _bs(kind):
+    from bs import BS
+    bg = S.background(kind)
+    bs = BS(len(bg["lon"]), len(bg["lat"]))
+    bs.load_arrays(**bg)
+    bs.ready(xcyclic=True)
+    return bs, bg
+
+
+def _engine(kind):
+    from engine import RayEngine
+    bs, bg = _bs(kind)
+    return RayEngine.from_bs(bs), bg
+
+
+def _gpu_rows(eng, y0, nt, chunk):
+    rows = {}
+    res = eng.integrate(torch.as_tensor(y0), nt, 7200.0, ttotal=(nt - 1) * 7200.0, chunk=chunk,
+                        sink=lambda a, b, o: rows.__setitem__((a, b), o.cpu().numpy().copy()))
+    nray = y0.shape[1]
+    hist = np.full((nray, nt, 8), np.nan)
+    for (i0, i1), r in rows.items():
+        hist[:, i0:i1] = r
+    return hist, res
+
+
+def _oracle(bg, y0, nt):
+    import rwrt_oracle as O
+    try:
+        O._devmath_lib()
+    except (RuntimeError, OSError) as e:
+        pytest.skip(f"oracle/_devmath not built: {e}")
+    with np.errstate(all="ignore"), O.device_math():
+        hist, nacc, nrej, status = O.ray_run(O.Background(**bg), y0.copy(), nt, 7200.0)
+    return hist, nacc, nrej, status
+
+
+def _same(a, b):
+    a = np.where(np.isnan(a), np.nan, a)
+    b = np.where(np.isnan(b), np.nan, b)
+    return np.array_equal(a.view(np.int64), b.view(np.int64))
+
+
+def _check(hist, res, ref, nrow=None):
+    h, nacc, nrej, status = ref
+    nrow = nrow or h.shape[1]
+    g = np.transpose(hist[:, 1:nrow, :7], (2, 1, 0))        # (7, rows 1.., ray)
+    assert _same(g, h[:, 1:nrow])
+    assert np.array_equal(res.nacc.cpu().numpy(), nacc)
+    assert np.array_equal(res.nrej.cpu().numpy(), nrej)
+
+
+def test_empty_batch():
+    eng, _ = _engine("zonal")
+    hist, res = _gpu_rows(eng, np.zeros((5, 0)), NT, 7)
+    assert hist.shape == (0, NT, 8)
+    assert res.nacc.numel() == 0 and res.ray_steps == 0 and res.n_live == 0
+    assert not res.failed
+
+
+@pytest.mark.parametrize("n", [1, 127, 129, 300])
+def test_ragged_batches_bitwise(n):
+    eng, bg = _engine("nonzonal")
+    rows = golden("init_C2_nonzonal.npz")["rows"][:5].reshape(5, -1)
+    rng = np.random.default_rng(n)
+    live = np.flatnonzero(~np.isnan(rows.sum(0)))
+    dead = np.flatnonzero(np.isnan(rows.sum(0)))
+    k = max(1, n // 3)                       # a third dead slots, the rest live
+    pick = np.concatenate([rng.choice(dead, min(k, n - 1) if n > 1 else 0, replace=False),
+                           rng.choice(live, n - (min(k, n - 1) if n > 1 else 0), replace=False)])
+    rng.shuffle(pick)
+    y0 = np.ascontiguousarray(rows[:, pick])
+    hist, res = _gpu_rows(eng, y0, NT, 7)
+    _check(hist, res, _oracle(bg, y0, NT))
+
+
+def test_all_frozen_batch_bitwise():
+    eng, bg = _engine("zonal")
+    rows = golden("init_C2_zonal.npz")["rows"][:5].reshape(5, -1)
+    dead = np.flatnonzero(np.isnan(rows.sum(0)))
+    assert len(dead) > 300
+    y0 = np.ascontiguousarray(rows[:, dead[:300]])
+    assert np.isfinite(y0[:2]).all()         # dead roots keep their source position
+    hist, res = _gpu_rows(eng, y0, NT, 7)
+    ref = _oracle(bg, y0, NT)
+    _check(hist, res, ref)
+    assert res.ray_steps == 0 and res.break_row is None
+    # every row is the source position with NaN wavenumbers, ug, vg
+    assert _same(hist[:, 1:, :2], np.broadcast_to(y0[:2].T[:, None, :], (300, NT - 1, 2)))
+
+
+def test_all_nan_batch_breaks_at_row_1():
+    eng, bg = _engine("zonal")
+    y0 = np.full((5, 200), np.nan)
+    hist, res = _gpu_rows(eng, y0, NT, 7)
+    assert res.break_row == 1 and res.ray_steps == 0
+    h, _, _, _ = _oracle(bg, y0, NT)
+    assert np.isnan(h[:, 1:]).all()
