@@ -161,7 +161,8 @@ rwrt_status rwrt_rk45_init(const rwrt_grid* g, const double* d_packed,
  * library-owned scratch (1 byte per ray per device, grown on demand) and
  * their rows written by a kernel on a library side stream; `stream` waits
  * for it, so the call remains one stream-ordered operation (also for
- * rwrt_rk45_run_tv). */
+ * rwrt_rk45_run_tv).  Calls on different streams of one device are
+ * serialised on the device (each waits for the previous call's end). */
 rwrt_status rwrt_rk45_run(const rwrt_grid* g, const double* d_packed,
                           int64_t nray, const rwrt_params* p,
                           const double* d_tbound, int32_t it_begin,

@@ -2175,6 +2175,8 @@ struct FillScratch {
   size_t cap = 0;
   hipStream_t side = nullptr;
   hipEvent_t flagged = nullptr, filled = nullptr;
+  hipEvent_t done = nullptr;   // end of the last call: calls on other streams wait for it
+  bool used = false;
 };
 FillScratch* fill_scratch(int64_t nray) {
   static FillScratch cache[64];
@@ -2184,7 +2186,8 @@ FillScratch* fill_scratch(int64_t nray) {
   if (!f.side) {
     if (hipStreamCreateWithFlags(&f.side, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&f.flagged, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&f.filled, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&f.filled, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&f.done, hipEventDisableTiming) != hipSuccess) {
       f.side = nullptr;
       return nullptr;
     }
@@ -2236,6 +2239,10 @@ rwrt_status launch_run(const BG& B, int64_t nray, const rwrt_params* p, const do
   FillScratch* fs = fill_scratch(nray);
   if (!fs) return fail(RWRT_ERR_HIP, "frozen-ray scratch allocation failed%s");
   a.frozen = fs->flags;
+  // the flags are shared by every call on this device: a call on another
+  // stream must not overwrite them while an earlier call still reads them
+  if (fs->used && hipStreamWaitEvent((hipStream_t)stream, fs->done, 0) != hipSuccess)
+    return check_launch("hipStreamWaitEvent(previous call)");
   hipLaunchKernelGGL(frozen_flag_kernel, dim3(grid_for(nray, 256)), dim3(256), 0, (hipStream_t)stream,
                      d_state, nray, fs->flags);
   if (rwrt_status s = check_launch("frozen_flag_kernel")) return s;
@@ -2250,8 +2257,10 @@ rwrt_status launch_run(const BG& B, int64_t nray, const rwrt_params* p, const do
                      dim3(kFillThreads), 0, fs->side, a);
   if (rwrt_status s = check_launch("frozen_fill_kernel")) return s;
   if (hipEventRecord(fs->filled, fs->side) != hipSuccess ||
-      hipStreamWaitEvent((hipStream_t)stream, fs->filled, 0) != hipSuccess)
+      hipStreamWaitEvent((hipStream_t)stream, fs->filled, 0) != hipSuccess ||
+      hipEventRecord(fs->done, (hipStream_t)stream) != hipSuccess)
     return check_launch("hipEventRecord(frozen fill)");
+  fs->used = true;
 #endif
   return RWRT_OK;
 }

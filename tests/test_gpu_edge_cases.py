@@ -118,3 +118,24 @@ def test_all_nan_batch_breaks_at_row_1():
     assert res.break_row == 1 and res.ray_steps == 0
     h, _, _, _ = _oracle(bg, y0, NT)
     assert np.isnan(h[:, 1:]).all()
+
+
+def test_calls_on_two_streams_equal_one_stream():
+    """The library's frozen-ray scratch is per device: calls issued on two
+    streams (two engines) wait for each other and give the same rows."""
+    rows = golden("init_C2_nonzonal.npz")["rows"][:5].reshape(5, -1)
+    y0 = torch.as_tensor(np.ascontiguousarray(rows), device="cuda")
+    nray = y0.shape[1]
+    ref, _ = _gpu_rows(_engine("nonzonal")[0], rows, NT, 7)
+    outs = []
+    for _ in range(2):
+        eng = _engine("nonzonal")[0]
+        s = torch.cuda.Stream()
+        with torch.cuda.stream(s):
+            out = torch.empty((nray, NT - 1, 8), dtype=torch.float64, device="cuda")
+            eng.integrate(y0, NT, 7200.0, ttotal=(NT - 1) * 7200.0, chunk=6, out=[out])
+            outs.append(out)
+    torch.cuda.synchronize()
+    for out in outs:   # the buffer holds the last 6-row chunk (rows 19..24)
+        last = out.reshape(-1)[: nray * 6 * 8].reshape(nray, 6, 8).cpu().numpy()
+        assert _same(last, ref[:, NT - 6:])
