@@ -386,12 +386,13 @@ def main_c5(args, dist, rank, world, dev):
     y0 = make_y0()
     nslot = y0.shape[1]
     n_live = int((~torch.isnan(y0.sum(0))).sum().item())
-    # rows per launch (measured, profiles/r1/c5/chunk_sweep.txt): fp64 levels want a
-    # short time window (4 days: 17 levels in flight), fp32 levels the longest
-    # launches the output buffer allows (fewer launch tails beat locality)
+    # rows per launch (measured, profiles/r1/c5/chunk_sweep.txt and
+    # profiles/r1/v7/c5/): fp64 levels want a short time window (4 days: 17
+    # levels in flight), fp32 levels 20-day windows (240 rows: 1.11e9 against
+    # 1.07e9 for one 1080-row launch and 1.01e9 for 480 rows at 90 d)
     free = torch.cuda.mem_get_info(dev)[0]
     cap = max(1, min(nt - 1, int(0.8 * free) // (nslot * 64)))
-    chunk = min(args.chunk or (cap if lv.fp32 else 48), cap)
+    chunk = min(args.chunk or (240 if lv.fp32 else 48), cap)
     out = torch.empty((nslot, min(chunk, nt - 1), 8), dtype=torch.float64, device=dev)
 
     def one_step(events=None):
