@@ -1872,8 +1872,17 @@ struct Rk4Args {
   int32_t* queue;
 };
 
+#ifndef RWRT_RK4_CACHE
+#define RWRT_RK4_CACHE 1   // the RHS lookups through rk45_run_kernel's per-lane LDS cell cache
+#endif
 __global__ void __launch_bounds__(256, RWRT_WAVES_PER_SIMD) rk4_run_kernel(Rk4Args a) {
   const int64_t nrows = a.it_end - a.it_begin;
+#if RWRT_RK4_CACHE
+  __shared__ __attribute__((aligned(16))) char smem[LaneBG<StaticBG>::kLdsBytes];
+  const auto RB = LaneBG<StaticBG>::make(StaticBG{a.F}, smem);
+#else
+  const StaticBG RB{a.F};
+#endif
   const double half = 0.5 * a.dt;        // 0.5 * dt      (wr.py:602-604)
   const double sixth = a.dt / 6.0;       // dt / 6.0      (wr.py:92)
   for (;;) {
@@ -1898,7 +1907,7 @@ __global__ void __launch_bounds__(256, RWRT_WAVES_PER_SIMD) rk4_run_kernel(Rk4Ar
 #pragma unroll
         for (int v = 0; v < 5; ++v) ys[v] = (s == 0) ? y[v] : y[v] + c * k[v];
         if (s > 0 && rhs_bad(ys)) held = true;
-        ray_rhs(StaticBG{a.F}, 0.0, ys, k);
+        ray_rhs(RB, 0.0, ys, k);
         const double wgt = (s == 1 || s == 2) ? 2.0 : 1.0;
 #pragma unroll
         for (int v = 0; v < 5; ++v) acc[v] = (s == 0) ? k[v] : acc[v] + wgt * k[v];
