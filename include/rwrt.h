@@ -177,8 +177,10 @@ rwrt_status rwrt_rk45_run(const rwrt_grid* g, const double* d_packed,
  * p->tstep.  A ray whose stage input is masked (|lat| >= pi/2 or |l| >= 100)
  * keeps its state for that step.  d_state rows 0..4 hold y (set them to the
  * initial rows before the first call); d_count[nray][2] = {steps taken, steps
- * held}; d_nanrow / d_out / d_work as for rwrt_rk45_run (nacc column = steps
- * taken). */
+ * held} (the step of a state with a NaN in lon/lat/k/l is not counted);
+ * d_nanrow / d_out / d_work as for rwrt_rk45_run (nacc column = steps
+ * taken); rays with such a NaN at the call's start are written from the
+ * library's side stream as in rwrt_rk45_run. */
 rwrt_status rwrt_rk4_run(const rwrt_grid* g, const double* d_packed,
                          int64_t nray, const rwrt_params* p, int32_t it_begin,
                          int32_t it_end, const int64_t* d_order,

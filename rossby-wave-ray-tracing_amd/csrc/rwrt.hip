@@ -1870,6 +1870,7 @@ struct Rk4Args {
   int32_t* nanrow;
   double* out;
   int32_t* queue;
+  const uint8_t* frozen;   // rays whose rows rk4_fill_kernel writes (NULL: none)
 };
 
 #ifndef RWRT_RK4_CACHE
@@ -1889,6 +1890,7 @@ __global__ void __launch_bounds__(256, RWRT_WAVES_PER_SIMD) rk4_run_kernel(Rk4Ar
     const int32_t w = atomicAdd(a.queue, 1);
     if (w >= a.nray) break;
     const int64_t ray = a.order ? a.order[w] : (int64_t)w;
+    if (a.frozen && a.frozen[ray]) continue;   // its rows come from rk4_fill_kernel
     double y[5];
 #pragma unroll
     for (int v = 0; v < 5; ++v) y[v] = a.state[v * a.nray + ray];
@@ -1899,6 +1901,9 @@ __global__ void __launch_bounds__(256, RWRT_WAVES_PER_SIMD) rk4_run_kernel(Rk4Ar
     while (it < a.it_end) {
       // one RK4 step: k1 at y; k2, k3 at y + dt/2 k; k4 at y + dt k3 (one RHS copy)
       const bool bad1 = rhs_bad(y);
+      // a state with a NaN in lon/lat/k/l is stepped (to all-NaN) but not
+      // counted: the count is then the same however the run is chunked
+      const bool nan_in = isnan(y[0]) || isnan(y[1]) || isnan(y[2]) || isnan(y[3]);
       bool held = bad1;
       double acc[5], k[5], ys[5];
 #pragma nounroll
@@ -1916,7 +1921,7 @@ __global__ void __launch_bounds__(256, RWRT_WAVES_PER_SIMD) rk4_run_kernel(Rk4Ar
       if (!held) {
 #pragma unroll
         for (int v = 0; v < 5; ++v) y[v] = y[v] + sixth * acc[v];
-        ++nstep;
+        nstep += nan_in ? 0 : 1;
       } else if (!bad1) {
         ++nhold;
       }
@@ -1954,6 +1959,84 @@ __global__ void __launch_bounds__(256, RWRT_WAVES_PER_SIMD) rk4_run_kernel(Rk4Ar
     a.count[2 * ray] = nstep;
     a.count[2 * ray + 1] = nhold;
     a.nanrow[ray] = nanrow;
+  }
+}
+
+// RK4 rays with a NaN in lon, lat, k or l at the launch start: their first
+// step either holds them (a masked first stage, wr.py:600) or makes the whole
+// state NaN (every derivative of such a state is NaN), and rk4_run_kernel
+// then repeats that row to the end of the chunk -- so these rays' rows are
+// known before the launch.  rk4_flag_kernel marks them, rk4_run_kernel skips
+// them and rk4_fill_kernel (side stream, beside the run kernel) applies that
+// step and the post-processing of wr.py:718-756 as the run kernel does and
+// writes the rows like frozen_fill_kernel.
+__global__ void rk4_flag_kernel(const double* __restrict__ state, int64_t nray,
+                                uint8_t* __restrict__ frozen) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nray;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    bool nan = false;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) nan = nan || isnan(state[v * nray + i]);
+    frozen[i] = nan ? 1 : 0;
+  }
+}
+
+__global__ void __launch_bounds__(kFillThreads) __attribute__((amdgpu_num_vgpr(128)))
+rk4_fill_kernel(Rk4Args a) {
+  __shared__ double2 rowbuf[kFillThreads][4];
+  __shared__ int list[kFillThreads];
+  __shared__ int cnt;
+  const int64_t nrows = a.it_end - a.it_begin;
+  const int64_t base = blockIdx.x * (int64_t)kFillThreads;
+  if (threadIdx.x == 0) cnt = 0;
+  __syncthreads();
+  const int64_t ray = base + threadIdx.x;
+  if (ray < a.nray && a.frozen[ray]) {
+    double y[5];
+#pragma unroll
+    for (int v = 0; v < 5; ++v) y[v] = a.state[v * a.nray + ray];
+    int64_t nstep = a.count[2 * ray];
+    int32_t nanrow = a.nanrow[ray];
+    const double prev_lon = y[0], prev_lat = y[1];
+    const int it = a.it_begin;
+    // rk4_run_kernel's step: held iff the first stage is masked; otherwise
+    // every stage derivative is NaN and so is y + dt/6 * acc (not counted)
+    if (!rhs_bad(y)) {
+#pragma unroll
+      for (int v = 0; v < 5; ++v) y[v] = kNaN;
+    }
+    if (fabs(y[1]) >= kHalfPi) {
+#pragma unroll
+      for (int v = 0; v < 5; ++v) y[v] = kNaN;
+    }
+    if (cal_dis(y[0], y[1], prev_lon, prev_lat) >= a.cut_off) {
+#pragma unroll
+      for (int v = 0; v < 5; ++v) y[v] = kNaN;
+    }
+    double ug, vg;
+    ugvg_at(StaticBG{a.F}, 0.0, y[0], y[1], y[2], y[3], ug, vg);
+    rowbuf[threadIdx.x][0] = make_double2(y[0], y[1]);
+    rowbuf[threadIdx.x][1] = make_double2(y[2], y[3]);
+    rowbuf[threadIdx.x][2] = make_double2(y[4], ug);
+    rowbuf[threadIdx.x][3] = make_double2(vg, (double)nstep);
+    if (nanrow == a.nt && isnan(y[0])) nanrow = it;
+#pragma unroll
+    for (int v = 0; v < 5; ++v) a.state[v * a.nray + ray] = y[v];
+    a.count[2 * ray] = nstep;
+    a.nanrow[ray] = nanrow;
+    list[atomicAdd(&cnt, 1)] = threadIdx.x;
+  }
+  __syncthreads();
+  const int n = cnt;
+  const int64_t nq = nrows * 4;
+  for (int k = 0; k < n; ++k) {
+    const int j = list[k];
+    double2* o = reinterpret_cast<double2*>(a.out + (size_t)(base + j) * nrows * RWRT_NOUT);
+    const double2 v = rowbuf[j][threadIdx.x & 3];
+    for (int64_t q = threadIdx.x; q < nq; q += kFillThreads) store_row16<RWRT_NT_FILL>(o + q, v);
+#if RWRT_FILL_THROTTLE
+    for (int64_t z = RWRT_FILL_THROTTLE; z <= nrows; z += RWRT_FILL_THROTTLE) __builtin_amdgcn_s_sleep(127);
+#endif
   }
 }
 
@@ -2599,12 +2682,38 @@ rwrt_status rwrt_rk4_run(const rwrt_grid* g, const double* d_packed, int64_t nra
   if (hipMemsetAsync(d_work, 0, sizeof(int32_t), (hipStream_t)stream) != hipSuccess)
     return check_launch("hipMemsetAsync(queue)");
   Rk4Args a{F, nray, p->tstep, p->cut_off, p->nt, it_begin, it_end, d_order, d_state, d_count,
-            d_nanrow, d_out, d_work};
+            d_nanrow, d_out, d_work, nullptr};
   int64_t blocks = persistent_blocks<StaticBG>();
   const int64_t need = (nray + 255) / 256;
   if (blocks > need) blocks = need;
+#if RWRT_FROZEN_FILL
+  // rays whose rows are known at the start go to rk4_fill_kernel on the side
+  // stream (as launch_run does for the RK45 loop)
+  FillScratch* fs = fill_scratch(nray);
+  if (!fs) return fail(RWRT_ERR_HIP, "frozen-ray scratch allocation failed%s");
+  a.frozen = fs->flags;
+  if (fs->used && hipStreamWaitEvent((hipStream_t)stream, fs->done, 0) != hipSuccess)
+    return check_launch("hipStreamWaitEvent(previous call)");
+  hipLaunchKernelGGL(rk4_flag_kernel, dim3(grid_for(nray, 256)), dim3(256), 0, (hipStream_t)stream,
+                     d_state, nray, fs->flags);
+  if (rwrt_status s = check_launch("rk4_flag_kernel")) return s;
+  if (hipEventRecord(fs->flagged, (hipStream_t)stream) != hipSuccess ||
+      hipStreamWaitEvent(fs->side, fs->flagged, 0) != hipSuccess)
+    return check_launch("hipEventRecord(rk4 flags)");
+#endif
   hipLaunchKernelGGL(rk4_run_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
-  return check_launch("rk4_run_kernel");
+  if (rwrt_status s = check_launch("rk4_run_kernel")) return s;
+#if RWRT_FROZEN_FILL
+  hipLaunchKernelGGL(rk4_fill_kernel, dim3((unsigned)((nray + kFillThreads - 1) / kFillThreads)),
+                     dim3(kFillThreads), 0, fs->side, a);
+  if (rwrt_status s = check_launch("rk4_fill_kernel")) return s;
+  if (hipEventRecord(fs->filled, fs->side) != hipSuccess ||
+      hipStreamWaitEvent((hipStream_t)stream, fs->filled, 0) != hipSuccess ||
+      hipEventRecord(fs->done, (hipStream_t)stream) != hipSuccess)
+    return check_launch("hipEventRecord(rk4 fill)");
+  fs->used = true;
+#endif
+  return RWRT_OK;
 }
 
 rwrt_status rwrt_kat_rk45(int32_t kind, int64_t ncol, const double* d_y0, int32_t nt,

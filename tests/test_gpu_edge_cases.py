@@ -139,3 +139,35 @@ def test_calls_on_two_streams_equal_one_stream():
     for out in outs:   # the buffer holds the last 6-row chunk (rows 19..24)
         last = out.reshape(-1)[: nray * 6 * 8].reshape(nray, 6, 8).cpu().numpy()
         assert _same(last, ref[:, NT - 6:])
+
+
+def test_rk4_chunked_runs_equal_one_launch():
+    """RK4 rays with a NaN in lon/lat/k/l at a launch start are written by
+    rk4_fill_kernel; 40-row chunks (rays dying in one chunk enter the next one
+    flagged) equal one launch bit for bit, and the oracle's RK4 rows."""
+    import rwrt_oracle as O
+    eng, bg = _engine("nonzonal")
+    g = golden("init_C2_nonzonal.npz")
+    rows7 = g["rows"].reshape(7, -1)
+    y0 = torch.as_tensor(np.ascontiguousarray(rows7[:5]), device="cuda")
+    nt = 241
+    res = {}
+    for chunk in (None, 40):
+        got = {}
+        r = eng.integrate_rk4(y0, nt, 7200.0, chunk=chunk,
+                              sink=lambda a, b, o: got.__setitem__((a, b), o.cpu().numpy().copy()))
+        h = np.full((y0.shape[1], nt, 8), np.nan)
+        for (i0, i1), v in got.items():
+            h[:, i0:i1] = v
+        res[chunk] = (h, r)
+    (h1, r1), (h2, r2) = res[None], res[40]
+    assert _same(h1[:, 1:], h2[:, 1:])
+    assert torch.equal(r1.nacc, r2.nacc) and torch.equal(r1.nrej, r2.nrej)
+    assert torch.equal(r1.nanrow, r2.nanrow)
+    try:
+        O._devmath_lib()
+    except (RuntimeError, OSError) as e:
+        pytest.skip(f"oracle/_devmath not built: {e}")
+    with np.errstate(all="ignore"), O.device_math():
+        href, _ = O.ray_run_rk4(O.Background(**bg), rows7[:5].copy(), nt, 7200.0, row0=rows7)
+    assert _same(np.transpose(h2[:, 1:, :7], (2, 1, 0)), href[:, 1:])

@@ -37,7 +37,7 @@ def main():
         res = eng.integrate_rk4(y0, nt, 7200.0, out=out)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / a.steps
-    live = ~torch.isnan(y0.sum(0))      # NaN states count one step per launch: left out
+    live = ~torch.isnan(y0.sum(0))      # dead slots (NaN roots) take no counted steps
     steps = int(res.nacc[live].sum().item())
     print(json.dumps({"workload": f"C3 RK4, {a.days:g} d at 2 h", "slots": int(y0.shape[1]),
                       "live": int(live.sum().item()), "rk4_steps": steps, "s_per_run": dt,
