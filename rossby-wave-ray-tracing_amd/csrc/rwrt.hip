@@ -1745,7 +1745,10 @@ __global__ void frozen_flag_kernel(const double* __restrict__ state, int64_t nra
 // beside the run kernel's 146 KB, or the fill would wait for the run to end.
 constexpr int kFillThreads = 128;
 #ifndef RWRT_FILL_THROTTLE
-#define RWRT_FILL_THROTTLE 256
+#define RWRT_FILL_THROTTLE 64
+#endif
+#ifndef RWRT_FILL_SLEEP      // s_sleep units (64 clocks) per RWRT_FILL_THROTTLE rows
+#define RWRT_FILL_SLEEP 32
 #endif
 template <class BG>
 __global__ void __launch_bounds__(kFillThreads) __attribute__((amdgpu_num_vgpr(128)))
@@ -1806,10 +1809,10 @@ frozen_fill_kernel(RunArgs<BG> a) {
     const double2 v = rowbuf[j][threadIdx.x & 3];
     for (int64_t q = threadIdx.x; q < nq; q += kFillThreads) store_row16<RWRT_NT_FILL>(o + q, v);
 #if RWRT_FILL_THROTTLE
-    // pace the stores (~4 us per full RWRT_FILL_THROTTLE rows; none for short
+    // pace the stores (~0.9 us per full 64 rows written; none for shorter
     // chunks): a full-rate fill floods the memory queues the run kernel's
     // lookups wait in
-    for (int64_t z = RWRT_FILL_THROTTLE; z <= nrows; z += RWRT_FILL_THROTTLE) __builtin_amdgcn_s_sleep(127);
+    for (int64_t z = RWRT_FILL_THROTTLE; z <= nrows; z += RWRT_FILL_THROTTLE) __builtin_amdgcn_s_sleep(RWRT_FILL_SLEEP);
 #endif
   }
 }
@@ -2035,7 +2038,7 @@ rk4_fill_kernel(Rk4Args a) {
     const double2 v = rowbuf[j][threadIdx.x & 3];
     for (int64_t q = threadIdx.x; q < nq; q += kFillThreads) store_row16<RWRT_NT_FILL>(o + q, v);
 #if RWRT_FILL_THROTTLE
-    for (int64_t z = RWRT_FILL_THROTTLE; z <= nrows; z += RWRT_FILL_THROTTLE) __builtin_amdgcn_s_sleep(127);
+    for (int64_t z = RWRT_FILL_THROTTLE; z <= nrows; z += RWRT_FILL_THROTTLE) __builtin_amdgcn_s_sleep(RWRT_FILL_SLEEP);
 #endif
   }
 }
