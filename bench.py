@@ -1,21 +1,30 @@
 """Benchmark: RK45 ray-steps/s of the MI355X ray integrator (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--days D]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--days D] [--bg zonal|nonzonal]
 
-One "step" = one pass of the hot path over one batch: the whole C3 workload
+One "step" = one pass of the hot path over ONE ray set: the whole C3 workload
 (2-degree global seed grid x k = 1..10 x periods {inf, 50, 30, 20, 10} d =
-2.40 M ray slots, of which ~0.7 M have a real initial root) integrated for
-90 days (1081 output rows at 2 h) -- solver construction, the ray loop and
-every output row included.  Inputs are resident in HBM when the timed region
-starts.  For N > 1 each rank (one per GPU, launched by torch.distributed.run)
-integrates its own C3-sized batch (sources shifted by r*2/N degrees of
-longitude): per-GPU work is fixed, rays never interact, no collective runs
-inside the timed region (scaling "weak").
+2.40 M ray slots, of which 0.72 M have a real initial root) integrated for 90
+days (1081 output rows at 2 h) -- GPU initial rows, solver construction, the
+ray loop and every output row included.  Inputs are resident in HBM when the
+timed region starts.
+
+With N ranks (one per GPU, torch.distributed.run; BASELINE configs[3] = C4)
+the SAME set is split across the GPUs (shard.run_sharded, scaling "strong"):
+inside each timed step rank 0's basic state is broadcast over RCCL, every rank
+builds the initial rows and runs a 6-row probe launch over every ray, the
+probe's per-ray attempts decide a cost-balanced split (no communication: the
+same deterministic rule on every rank), each rank integrates its own rays to
+90 days, and the last row and step counters of every ray are gathered to
+rank 0 over RCCL.  value = the set's accepted ray-steps / the slowest rank's
+wall time.
 
 Rank 0 prints ONE JSON line.  ``roofline`` prices the ray-loop kernel at the
-algorithmic 2112 B per accepted ray-step; ``cpu_baseline``
-times the NumPy oracle (oracle/rwrt_oracle.py, bit-exact with the reference)
-on a bounded sample of the same rays on the host.
+bound it actually hits -- VALU instruction issue at one wave per SIMD (PMC
+SQ_INSTS_VALU x 4 cycles against 1024 SIMDs x the in-kernel clock) -- with the
+real HBM traffic (PMC) and the algorithmic 2112 B per ray-step of SURVEY.md
+§8(d) beside it; ``cpu_baseline`` times the NumPy oracle (oracle/rwrt_oracle.py,
+bit-exact with the reference) on a bounded sample of the same rays on the host.
 """
 import argparse
 import json
@@ -86,7 +95,7 @@ def cpu_baseline(bg, y0, nrays, days, seed=0):
     with np.errstate(all="ignore"):
         hist, nacc, nrej, st = O.ray_run(ob, y0[:, pick].copy(), nt, 7200.0)
     dt = time.perf_counter() - t0
-    return pick, hist, int(nacc.sum()), dt, nt
+    return pick, hist, int(nacc.sum()), dt, nt, int(nrej.sum())
 
 
 def cpu_baseline_mp(bg, y0, procs, rays_per_proc, days, seed=1):
@@ -128,13 +137,13 @@ def devmath_check(bg, y0, pick, gpu, nt, nrays=2048):
             "rays_identical_all_rows": int(same.all(axis=(0, 1)).sum())}
 
 
-def find_traffic(path, workload, schedule):
-    """Per-launch HBM bytes of the ray kernel from a PMC profile of this workload
-    run with the same launch schedule (rows per launch)."""
+def find_profile(name, path, workload, schedule):
+    """A per-launch profile summary (profiles/<round>/.../<name>) of this
+    workload run with the same launch schedule (rows per launch)."""
     import glob
     # newest profile first by path (profiles/<round>/<version>/...: sorts the
     # same in any checkout, unlike file times)
-    cands = [path] if path else sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "traffic.json"), recursive=True),
+    cands = [path] if path else sorted(glob.glob(os.path.join(ROOT, "profiles", "**", name), recursive=True),
                                        reverse=True)
     for c in cands:
         try:
@@ -144,6 +153,39 @@ def find_traffic(path, workload, schedule):
         if t.get("workload") == workload and t.get("launch_rows") == schedule:
             return t, os.path.relpath(c, ROOT)
     return None, None
+
+
+def roofline(steps_per_launch, avg_launch_s, workload, schedule, bytes_per_step, args):
+    """The ray-loop kernel against the bound it hits: VALU issue at one wave per
+    SIMD.  VALU wave-instructions per launch and the in-kernel clock come from
+    the PMC profile of this build and schedule (tools/pmc_valu.py), the launch
+    time from this run's HIP events.  Real HBM bytes (PMC) and the algorithmic
+    bytes of SURVEY.md §8(d) are reported beside it."""
+    valu, vsrc = find_profile("valu.json", args.valu_profile, workload, schedule)
+    traffic, tsrc = find_profile("traffic.json", args.traffic, workload, schedule)
+    alg = steps_per_launch * bytes_per_step / avg_launch_s
+    out = {"bound": "valu_issue", "achieved": None, "peak": None, "unit": "G VALU wave-instructions/s",
+           "frac": None, "traffic": traffic["traffic_bytes_per_launch"] if traffic else None,
+           "kernel": "rk45_run_kernel", "avg_launch_ms": 1e3 * avg_launch_s,
+           "valu_source": vsrc, "traffic_source": tsrc}
+    if valu:
+        ach = valu["valu_insts_per_launch"] / avg_launch_s
+        peak = valu["simds"] * valu["clock_hz"] / valu["cycles_per_valu"]
+        out.update(achieved=ach / 1e9, peak=peak / 1e9, frac=ach / peak,
+                   valu_insts_per_launch=valu["valu_insts_per_launch"],
+                   clock_GHz=valu["clock_hz"] / 1e9,
+                   note=("one wave per SIMD (256 VGPR + AGPRs, 146 KB LDS per block): every VALU "
+                         "wave-instruction holds its SIMD's issue for >= 4 cycles; peak = 1024 SIMDs x "
+                         "in-kernel clock (GRBM_GUI_ACTIVE / 8 / kernel time) / 4"))
+    out["hbm"] = {"achieved_GBps": traffic["traffic_bytes_per_launch"] / avg_launch_s / 1e9 if traffic else None,
+                  "peak_GBps": HBM_PEAK / 1e9,
+                  "frac": traffic["traffic_bytes_per_launch"] / avg_launch_s / HBM_PEAK if traffic else None,
+                  "unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)"}
+    out["algorithmic"] = {"bytes_per_ray_step": bytes_per_step, "GBps": alg / 1e9,
+                          "note": ("SURVEY.md 8(d): 6 RHS x 4 corners x 11 fields x 8 B per accepted step; "
+                                   "most lookups are served by the per-lane LDS cell cache and L2, so this "
+                                   "is a yardstick, not HBM traffic, and can exceed the HBM peak")}
+    return out
 
 
 def main():
@@ -159,22 +201,24 @@ def main():
     ap.add_argument("--cpu-procs", type=int, default=16,
                     help="processes of the multi-core CPU baseline (1: skip it)")
     ap.add_argument("--periods", type=int, default=5, help="C3 periods in the batch (1-5)")
+    ap.add_argument("--bg", default="zonal", choices=["zonal", "nonzonal"],
+                    help="C3 basic state: the DJF jets (SURVEY.md 8(d)) or their non-zonal variant")
     ap.add_argument("--order", default="priority", choices=["priority", "cost", "live"],
                     help="work-queue order: heaviest rays to high-priority waves (priority), "
                          "longest-first (cost), or live-first")
-    ap.add_argument("--first-chunk", default="6,24,96",
-                    help="rows of the short leading launches that measure per-ray cost (comma list)")
-    ap.add_argument("--init", default="gpu", choices=["gpu", "host"],
-                    help="initial rows: GPU kernel inside each step (default) or host rows resident")
+    ap.add_argument("--probe", type=int, default=6,
+                    help="rows of the probe launch over every ray whose attempts split and order the set")
+    ap.add_argument("--first-chunk", default="24,96",
+                    help="rows of the short launches after the probe that re-measure per-ray cost")
     ap.add_argument("--config", default="C3", choices=["C3", "C5"],
-                    help="C3 (BASELINE configs[2], the metric's workload) or C5 (configs[4]: "
-                         "0.25-degree time-varying background, ~3.9 M ray slots)")
+                    help="C3 (BASELINE configs[2]/[3], the metric's workload) or C5 (configs[4]: "
+                         "0.25-degree time-varying background)")
     ap.add_argument("--fields", default="fp64", choices=["fp64", "fp32"],
                     help="C5: storage of the background levels (arithmetic is fp64 either way)")
+    ap.add_argument("--c5-periods", type=int, default=2, help="C5 periods (1-5 of the C3 list)")
     ap.add_argument("--lib", default=None, help="alternative librwrt build (A/B timing)")
-    ap.add_argument("--traffic", default=None,
-                    help="traffic.json from tools/pmc_traffic.py (default: newest profiles/*/traffic.json "
-                         "for this workload)")
+    ap.add_argument("--traffic", default=None, help="traffic.json (tools/pmc_traffic.py)")
+    ap.add_argument("--valu-profile", default=None, help="valu.json (tools/pmc_valu.py)")
     ap.add_argument("--replicate", type=int, default=1,
                     help="diagnostic: repeat the ray batch k times (more rays per lane)")
     args = ap.parse_args()
@@ -184,7 +228,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
+    dist = group = None
     if world > 1:
         import torch.distributed as dist
         # one GPU per rank; RWRT_DIST_BACKEND=gloo with fewer GPUs than ranks
@@ -192,16 +236,17 @@ def main():
         local = local % max(torch.cuda.device_count(), 1)
         torch.cuda.set_device(local)
         dist.init_process_group(os.environ.get("RWRT_DIST_BACKEND", "nccl"))
+        group = dist.group.WORLD
     dev = torch.device("cuda", local if world > 1 else 0)
 
     if args.config == "C5":
-        return main_c5(args, dist, rank, world, dev)
+        return main_c5(args, dist, group, rank, world, dev)
     from engine import RayEngine
-    bs, bg = make_bs("zonal")
+    from shard import run_sharded
+    bs, bg = make_bs(args.bg)
     periods = S.C3_PERIODS_DAYS[: args.periods]
-    lon_off = rank * 2.0 / max(world, 1)
     t_init = time.perf_counter()
-    y0 = c3_initial_state(bs, lon_offset_deg=lon_off, periods=periods)
+    y0 = c3_initial_state(bs, periods=periods)
     t_init = time.perf_counter() - t_init
     if args.replicate > 1:
         y0 = np.concatenate([y0] * args.replicate, axis=1)
@@ -209,10 +254,10 @@ def main():
     n_live = int(np.sum(~np.isnan(y0.mean(axis=0))))
     eng = RayEngine.from_bs(bs, device=dev)
     nt = int(round(args.days * 12)) + 1
-    gpu_init = args.init == "gpu" and args.replicate == 1
+    gpu_init = args.replicate == 1
     if gpu_init:
         # sources and per-k constants resident in HBM; the step starts from them
-        src, zcs = c3_sources(eng, lon_off, periods)
+        src, zcs = c3_sources(eng, 0.0, periods)
         init_rows = [None] * len(zcs)
         init_info = torch.zeros(1, dtype=torch.int32, device=dev)
 
@@ -228,17 +273,22 @@ def main():
     else:
         init_same = None
         y0_d = torch.as_tensor(y0, device=dev)
-    # the whole history stays in HBM when it fits (C3: 166 GB of 288 GB), so
-    # the ray loop is a few launches: short cost probes, then all the rest
+    # this rank's rows stay in HBM (C3 on one GPU: 166 GB of 288 GB), so the
+    # ray loop is a few launches: the probe, two short re-ordering launches,
+    # then all the rest
+    n_local = -(-nslot // world) + 2                 # shard size bound (cost_partition)
     free = torch.cuda.mem_get_info(dev)[0]
-    chunk = args.chunk or max(1, min(nt - 1, int(0.8 * free) // (nslot * 64)))
-    out = torch.empty((nslot, min(chunk, nt - 1), 8), dtype=torch.float64, device=dev)
+    chunk = args.chunk or max(1, min(nt - 1, int(0.8 * free) // (n_local * 64)))
+    out = torch.empty((n_local, min(chunk, nt - 1), 8), dtype=torch.float64, device=dev)
+    lead = [int(x) for x in str(args.first_chunk).split(",") if x]
 
     def one_step(events=None):
+        if dist is not None:
+            dist.broadcast(eng.packed, 0, group=group)   # rank 0's basic state (RCCL over xGMI)
         y = make_y0() if gpu_init else y0_d
-        return eng.integrate(y, nt, 7200.0, ttotal=(nt - 1) * 7200.0, chunk=chunk, out=out,
-                             events=events, order_policy=args.order,
-                             first_chunk=[int(x) for x in str(args.first_chunk).split(",") if x])
+        return run_sharded(eng, y, nt, 7200.0, group=group, probe=args.probe, lead=lead,
+                           chunk=chunk, out=out, events=events, ttotal=(nt - 1) * 7200.0,
+                           order_policy=args.order)
 
     for _ in range(args.warmup):
         one_step()
@@ -250,70 +300,67 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         r = one_step(events)
-        steps_done += r.ray_steps
+        steps_done += r.steps_local
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     kern_s = sum(a.elapsed_time(b) for a, b in events) / 1e3
-    rej = int(r.nrej.sum().item())
+    rej = int(r.res.nrej.sum().item())
+    n_mine = int(r.idx.numel())
 
-    tot_steps, max_el = steps_done, elapsed
+    tot_steps, max_el, tot_rej = steps_done, elapsed, rej
     if dist:
-        t = torch.tensor([float(steps_done), elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([float(steps_done), elapsed, float(rej)], dtype=torch.float64, device=dev)
         s = t.clone()
         dist.all_reduce(s, op=dist.ReduceOp.SUM)
         m = t.clone()
         dist.all_reduce(m, op=dist.ReduceOp.MAX)
-        tot_steps, max_el = s[0].item(), m[1].item()
+        tot_steps, max_el, tot_rej = s[0].item(), m[1].item(), s[2].item()
 
     result = None
     if rank == 0:
         value = tot_steps / max_el
         per_launch_steps = steps_done / max(len(events), 1)
         avg_launch_s = kern_s / max(len(events), 1)
-        achieved = per_launch_steps * BYTES_PER_STEP / avg_launch_s
         workload = (f"C3: 2deg global seeds x k=1..10 x {args.periods} periods, "
-                    f"{args.days:g} d at 2 h, 2.5deg DJF jet background (BASELINE configs[2])")
-        schedule = [b - a for a, b in r.bounds]
-        traffic, tsrc = find_traffic(args.traffic, workload, schedule)
+                    f"{args.days:g} d at 2 h, 2.5deg DJF jet background"
+                    + (" (non-zonal variant)" if args.bg == "nonzonal" else "")
+                    + (" (BASELINE configs[2])" if world == 1 else " (BASELINE configs[3]: C4)"))
+        schedule = [args.probe] + [b - a for a, b in r.res.bounds]
         result = {
             "metric": METRIC, "value": value, "unit": "ray-steps/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": 1e3 * max_el / args.steps, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "scaling": "strong", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
             "config": {"workload": workload,
-                       "ray_slots_per_gpu": nslot, "live_rays_per_gpu": n_live, "rows": nt,
-                       "rows_per_launch": chunk, "launch_rows": [b - a for a, b in r.bounds],
-                       "parallelism": f"rays sharded, {world} rank(s), 1 GPU each"},
-            "ray_steps_per_step": steps_done / args.steps,
-            "rejected_per_accepted": rej / max(r.ray_steps, 1),
+                       "ray_slots": nslot, "live_rays": n_live, "rows": nt,
+                       "rows_per_launch": chunk, "launch_rows": schedule,
+                       "rank0_rays": n_mine,
+                       "parallelism": (f"one ray set over {world} GPU(s): cost-balanced split by a "
+                                       f"{args.probe}-row probe, RCCL broadcast of the basic state and "
+                                       f"gather of endpoints + step counters inside the timed step")},
+            "ray_steps_per_step": tot_steps / args.steps,
+            "rejected_per_accepted": tot_rej * args.steps / max(tot_steps, 1),
             "host_init_s": t_init,
             "init": ("GPU rwrt_ray_initial inside every timed step (bit-identical to the host rows)"
                      if gpu_init else "host NumPy rows, outside the timed region"),
             "init_bitwise_vs_host": init_same,
             "queue_order": args.order,
             "library": os.path.basename(os.environ.get("RWRT_LIB", "librwrt.so")),
-            "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK,
-                         "traffic": traffic["traffic_bytes_per_launch"] if traffic else None,
-                         "traffic_rate_GBps": (traffic["traffic_bytes_per_launch"] / avg_launch_s / 1e9
-                                               if traffic else None),
-                         "algorithmic_note": ("algorithmic bytes per SURVEY.md 8(d), most served from the "
-                                              "LDS lookup cache and L2; traffic = real HBM bytes (PMC)"),
-                         "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
-                         "traffic_source": tsrc,
-                         "algorithmic_bytes_per_launch": per_launch_steps * BYTES_PER_STEP,
-                         "kernel": "rk45_run_kernel", "avg_launch_ms": 1e3 * avg_launch_s,
-                         "launches": len(events), "bytes_per_ray_step": BYTES_PER_STEP},
+            "roofline": roofline(per_launch_steps, avg_launch_s, workload, schedule, BYTES_PER_STEP, args),
         }
         if world == 1 and not args.no_cpu:
-            pick, hist, csteps, cdt, cnt = cpu_baseline(bg, y0, args.cpu_rays, args.cpu_days)
+            pick, hist, csteps, cdt, cnt, crej = cpu_baseline(bg, y0, args.cpu_rays, args.cpu_days)
+            evals = 6.0 * (csteps + crej) / max(csteps, 1)     # FSAL: 6 RHS columns per attempt
             result["cpu_baseline"] = {
                 "value": csteps / cdt, "unit": "ray-steps/s", "cores": 1, "kind": "port",
                 "sample": f"{len(pick)} live C3 rays x {args.cpu_days:g} d ({csteps} ray-steps, "
-                          f"{cdt:.1f} s) with oracle/rwrt_oracle.py (NumPy, bit-exact vs reference)",
+                          f"{cdt:.1f} s) with oracle/rwrt_oracle.py: the reference's arithmetic bit for "
+                          f"bit (NumPy), but FSAL -- {evals:.1f} RHS columns per accepted step where the "
+                          f"reference's loop evaluates 14.0 (SURVEY.md 3.3 probe)",
+                "reference_equivalent_value": csteps / cdt * evals / 14.0,
                 "host_cpus": os.cpu_count()}
             if args.cpu_procs > 1:
                 msteps, mwall, mrays = cpu_baseline_mp(bg, y0, args.cpu_procs, args.cpu_rays // 4,
@@ -329,13 +376,13 @@ def main():
                           sink=lambda a, b, o: rows.__setitem__(a, o[:, :, :7].cpu().numpy()))
             gpu = np.concatenate([rows[k] for k in sorted(rows)], axis=1)   # rows 1..cnt-1
             parity = []
-            for row in sorted({min(12, cnt - 1), min(48, cnt - 1), cnt - 1}):
+            for row in sorted({1, min(12, cnt - 1), min(48, cnt - 1), cnt - 1}):
                 g, c = gpu[:, row - 1, :2], hist[:2, row].T
                 ok = ~np.isnan(g).any(1) & ~np.isnan(c).any(1)
                 d = np.max(np.abs(g[ok] - c[ok]), axis=1) if ok.any() else np.zeros(1)
                 parity.append({"horizon_days": row / 12.0, "rays": int(ok.sum()),
                                "p50": float(np.median(d)), "p99": float(np.percentile(d, 99)),
-                               "max": float(d.max()),
+                               "max": float(d.max()), "frac_gt_1e-6": float(np.mean(d > 1e-6)),
                                "alive_mismatch": int(np.sum(np.isnan(g[:, 0]) != np.isnan(c[:, 0])))})
             result["max_dpos_vs_cpu_rad"] = parity
             result["bitwise_vs_cpu_devmath"] = devmath_check(bg, y0, pick, gpu, cnt)
@@ -345,15 +392,18 @@ def main():
         dist.destroy_process_group()
 
 
-def main_c5(args, dist, rank, world, dev):
-    """BASELINE configs[4] on one GPU per rank: a 0.25-degree time-varying
-    background (one level every 6 h, built on the device by rwrt_bs_ready,
-    fp64 or fp32 storage) and 1-degree global seeds x k = 1..10 x periods
-    {stationary, 10 d} (3.87 M ray slots), 90 days at 2 h.  One step = GPU
-    initial rows + the time-varying ray loop; levels and sources are resident
-    in HBM before the timed region.  Rays shard like C3 (weak scaling)."""
+def main_c5(args, dist, group, rank, world, dev):
+    """BASELINE configs[4]: a 0.25-degree time-varying background (one level
+    every 6 h, built on the device by rwrt_bs_ready, fp64 or fp32 storage) and
+    1-degree global seeds x k = 1..10 x ``--c5-periods`` of the C3 periods,
+    90 days at 2 h.  One step = GPU initial rows + the time-varying ray loop
+    over the whole set, split across the ranks like C3/C4 (run_sharded:
+    probe, cost-balanced split, gather of endpoints + counters); levels and
+    sources are resident in HBM before the timed region (each rank builds
+    the same levels from the same synthetic snapshots)."""
     from engine import RayEngine
     from levels import Levels
+    from shard import run_sharded
     res, dt_bg = 0.25, 6 * 3600.0
     nt = int(round(args.days * 12)) + 1
     nlev = int(np.ceil((nt - 1) * 7200.0 / dt_bg)) + 1
@@ -369,11 +419,11 @@ def main_c5(args, dist, rank, world, dev):
     cfg = S.config("C5")
     deg2rad = np.pi / 180.0
     ix, iy = np.meshgrid(np.arange(cfg.nnx), np.arange(cfg.nny))
-    lon_off = rank * 1.0 / max(world, 1)
-    lon = (((cfg.SW_lon + lon_off) % 360.0 + ix.ravel() * cfg.dlon) % 360.0) * deg2rad
+    lon = ((cfg.SW_lon % 360.0 + ix.ravel() * cfg.dlon) % 360.0) * deg2rad
     lat = (cfg.SW_lat + iy.ravel() * cfg.dlat) * deg2rad
     src = eng.sources(lon, lat)
-    zcs = [eng.zwn_tensor(cfg.zwn, S.c3_freq(P)) for P in S.C5_PERIODS_DAYS]
+    periods = S.C3_PERIODS_DAYS[: args.c5_periods]
+    zcs = [eng.zwn_tensor(cfg.zwn, S.c3_freq(P)) for P in periods]
     rows = [None] * len(zcs)
 
     def make_y0():
@@ -388,17 +438,18 @@ def main_c5(args, dist, rank, world, dev):
     n_live = int((~torch.isnan(y0.sum(0))).sum().item())
     # rows per launch (measured, profiles/r1/c5/chunk_sweep.txt and
     # profiles/r1/v7/c5/): fp64 levels want a short time window (4 days: 17
-    # levels in flight), fp32 levels 20-day windows (240 rows: 1.11e9 against
-    # 1.07e9 for one 1080-row launch and 1.01e9 for 480 rows at 90 d)
+    # levels in flight), fp32 levels 20-day windows
+    n_local = -(-nslot // world) + 2
     free = torch.cuda.mem_get_info(dev)[0]
-    cap = max(1, min(nt - 1, int(0.8 * free) // (nslot * 64)))
+    cap = max(1, min(nt - 1, int(0.8 * free) // (n_local * 64)))
     chunk = min(args.chunk or (240 if lv.fp32 else 48), cap)
-    out = torch.empty((nslot, min(chunk, nt - 1), 8), dtype=torch.float64, device=dev)
+    out = torch.empty((n_local, min(chunk, nt - 1), 8), dtype=torch.float64, device=dev)
+    lead = [int(x) for x in str(args.first_chunk).split(",") if x]
 
     def one_step(events=None):
-        return eng.integrate(make_y0(), nt, 7200.0, ttotal=(nt - 1) * 7200.0, chunk=chunk, out=out,
-                             events=events, order_policy=args.order,
-                             first_chunk=[int(x) for x in str(args.first_chunk).split(",") if x])
+        return run_sharded(eng, make_y0(), nt, 7200.0, group=group, probe=args.probe, lead=lead,
+                           chunk=chunk, out=out, events=events, ttotal=(nt - 1) * 7200.0,
+                           order_policy=args.order)
 
     for _ in range(args.warmup):
         one_step()
@@ -410,57 +461,45 @@ def main_c5(args, dist, rank, world, dev):
     t0 = time.perf_counter()
     for _ in range(args.steps):
         r = one_step(events)
-        steps_done += r.ray_steps
+        steps_done += r.steps_local
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     kern_s = sum(a.elapsed_time(b) for a, b in events) / 1e3
-    tot_steps, max_el = steps_done, elapsed
+    rej = int(r.res.nrej.sum().item())
+    tot_steps, max_el, tot_rej = steps_done, elapsed, rej
     if dist:
-        t = torch.tensor([float(steps_done), elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([float(steps_done), elapsed, float(rej)], dtype=torch.float64, device=dev)
         s, m = t.clone(), t.clone()
         dist.all_reduce(s, op=dist.ReduceOp.SUM)
         dist.all_reduce(m, op=dist.ReduceOp.MAX)
-        tot_steps, max_el = s[0].item(), m[1].item()
+        tot_steps, max_el, tot_rej = s[0].item(), m[1].item(), s[2].item()
     if rank == 0:
         fbytes = 4 if lv.fp32 else 8
         bps = 6 * 4 * 11 * fbytes * 2          # 6 RHS x 4 corners x 11 fields x 2 levels
         per_launch_steps = steps_done / max(len(events), 1)
         avg_launch_s = kern_s / max(len(events), 1)
-        achieved = per_launch_steps * bps / avg_launch_s
-        workload = (f"C5: 1deg global seeds x k=1..10 x 2 periods, {args.days:g} d at 2 h, 0.25deg "
-                    f"time-varying background ({nlev} levels every 6 h, {args.fields} storage; "
+        workload = (f"C5: 1deg global seeds x k=1..10 x {len(periods)} periods, {args.days:g} d at 2 h, "
+                    f"0.25deg time-varying background ({nlev} levels every 6 h, {args.fields} storage; "
                     f"BASELINE configs[4])")
-        schedule = [b - a for a, b in r.bounds]
-        traffic, tsrc = find_traffic(args.traffic, workload, schedule)
+        schedule = [args.probe] + [b - a for a, b in r.res.bounds]
         print(json.dumps({
             "metric": METRIC, "value": tot_steps / max_el, "unit": "ray-steps/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * max_el / args.steps,
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic",
-            "config": {"workload": workload, "ray_slots_per_gpu": nslot, "live_rays_per_gpu": n_live,
+            "config": {"workload": workload, "ray_slots": nslot, "live_rays": n_live,
                        "rows": nt, "levels": nlev, "field_storage": args.fields,
                        "level_bytes": int(lv.packed[0].numel() * lv.packed.element_size()),
                        "rows_per_launch": chunk, "launch_rows": schedule,
-                       "parallelism": f"rays sharded, {world} rank(s), 1 GPU each"},
-            "ray_steps_per_step": steps_done / args.steps,
-            "rejected_per_accepted": int(r.nrej.sum().item()) / max(r.ray_steps, 1),
+                       "parallelism": f"one ray set over {world} GPU(s) (run_sharded, as C3/C4)"},
+            "ray_steps_per_step": tot_steps / args.steps,
+            "rejected_per_accepted": tot_rej * args.steps / max(tot_steps, 1),
             "levels_build_s": t_build,
             "init": "GPU rwrt_ray_initial inside every timed step",
-            "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK,
-                         "traffic": traffic["traffic_bytes_per_launch"] if traffic else None,
-                         "traffic_rate_GBps": (traffic["traffic_bytes_per_launch"] / avg_launch_s / 1e9
-                                               if traffic else None),
-                         "algorithmic_note": ("algorithmic bytes per SURVEY.md 8(d), most served from the "
-                                              "LDS lookup cache and L2; traffic = real HBM bytes (PMC)"),
-                         "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
-                         "traffic_source": tsrc,
-                         "algorithmic_bytes_per_launch": per_launch_steps * bps,
-                         "kernel": "rk45_run_kernel", "avg_launch_ms": 1e3 * avg_launch_s,
-                         "launches": len(events), "bytes_per_ray_step": bps}}))
+            "roofline": roofline(per_launch_steps, avg_launch_s, workload, schedule, bps, args)}))
     if dist:
         dist.barrier()
         dist.destroy_process_group()

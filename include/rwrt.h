@@ -15,6 +15,14 @@
  *    the default stream).  Status codes report argument and launch errors;
  *    per-ray failure is data (NaN), exactly as in the reference.
  *  - fp64 throughout; the fields are the reference's 18-field stack.
+ *  - The ray-loop entry points (rwrt_rk45_run, rwrt_rk45_run_tv, rwrt_rk4_run)
+ *    take an execution context, rwrt_ctx, that owns the library's own scratch
+ *    (a per-ray frozen flag, a side stream and its events).  Nothing else in
+ *    the library holds state between calls: calls through DISTINCT contexts
+ *    are reentrant and may run concurrently on different streams or threads.
+ *    One context may be shared by threads (its calls are serialised on the
+ *    host) and used on several streams (a call waits on the device for the
+ *    context's previous call before reusing its scratch).
  */
 #ifndef RWRT_H
 #define RWRT_H
@@ -25,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RWRT_ABI_VERSION 1
+#define RWRT_ABI_VERSION 2
 #define RWRT_NFIELD_REF 18  /* BS.fields[..., 18]            (bs.py:349-368) */
 #define RWRT_NFIELD_PACK 12 /* 11 hot fields + 1 pad per grid point           */
 #define RWRT_NVAR 5         /* y = (lon, lat, k, l, amp)     (wr.py:768-776)  */
@@ -77,6 +85,13 @@ typedef struct {
   double dt;
 } rwrt_background;
 const char* rwrt_version(void);
+
+/* Execution context of the ray-loop entry points: created
+ * for one HIP device, destroyed when no call through it is pending (destroy
+ * waits for the last call's kernels before freeing its scratch). */
+typedef struct rwrt_ctx rwrt_ctx;
+rwrt_status rwrt_ctx_create(int32_t device, rwrt_ctx** out);
+rwrt_status rwrt_ctx_destroy(rwrt_ctx* ctx);
 /* Last error message of the calling thread ("" if none). */
 const char* rwrt_last_error(void);
 
@@ -157,13 +172,12 @@ rwrt_status rwrt_rk45_init(const rwrt_grid* g, const double* d_packed,
  * d_state / d_count / d_nanrow carry the per-ray solver state across calls
  * (time chunking).  d_work: >= 2 int32 of scratch (queue heads), reset by
  * this call on `stream`.  Results do not depend on the order or n_heavy.
- * Rays frozen at the call's start (NaN in their state) are flagged in
- * library-owned scratch (1 byte per ray per device, grown on demand) and
- * their rows written by a kernel on a library side stream; `stream` waits
- * for it, so the call remains one stream-ordered operation (also for
- * rwrt_rk45_run_tv).  Calls on different streams of one device are
- * serialised on the device (each waits for the previous call's end). */
-rwrt_status rwrt_rk45_run(const rwrt_grid* g, const double* d_packed,
+ * Rays frozen at the call's start (NaN in their state) are flagged in the
+ * context's scratch (1 byte per ray, grown on demand) and their rows written
+ * by a kernel on the context's side stream; `stream` waits for it, so the
+ * call remains one stream-ordered operation (also for rwrt_rk45_run_tv and
+ * rwrt_rk4_run). */
+rwrt_status rwrt_rk45_run(rwrt_ctx* ctx, const rwrt_grid* g, const double* d_packed,
                           int64_t nray, const rwrt_params* p,
                           const double* d_tbound, int32_t it_begin,
                           int32_t it_end, const int64_t* d_order,
@@ -177,11 +191,13 @@ rwrt_status rwrt_rk45_run(const rwrt_grid* g, const double* d_packed,
  * p->tstep.  A ray whose stage input is masked (|lat| >= pi/2 or |l| >= 100)
  * keeps its state for that step.  d_state rows 0..4 hold y (set them to the
  * initial rows before the first call); d_count[nray][2] = {steps taken, steps
- * held} (the step of a state with a NaN in lon/lat/k/l is not counted);
- * d_nanrow / d_out / d_work as for rwrt_rk45_run (nacc column = steps
- * taken); rays with such a NaN at the call's start are written from the
- * library's side stream as in rwrt_rk45_run. */
-rwrt_status rwrt_rk4_run(const rwrt_grid* g, const double* d_packed,
+ * held} -- held by a masked stage 2-4, or by a masked first stage, which
+ * holds the ray for every remaining step (the step of a state with a NaN in
+ * lon/lat/k/l is counted in neither); d_nanrow / d_out / d_work as for
+ * rwrt_rk45_run (nacc column = steps taken); rays with such a NaN at the
+ * call's start are written from the context's side stream as in
+ * rwrt_rk45_run. */
+rwrt_status rwrt_rk4_run(rwrt_ctx* ctx, const rwrt_grid* g, const double* d_packed,
                          int64_t nray, const rwrt_params* p, int32_t it_begin,
                          int32_t it_end, const int64_t* d_order,
                          double* d_state, int64_t* d_count, int32_t* d_nanrow,
@@ -209,7 +225,7 @@ rwrt_status rwrt_rk45_init_tv(const rwrt_grid* g, const rwrt_background* b,
                               const rwrt_params* p, double* d_state,
                               int64_t* d_count, int32_t* d_nanrow,
                               int32_t* d_live, int64_t* d_summary, void* stream);
-rwrt_status rwrt_rk45_run_tv(const rwrt_grid* g, const rwrt_background* b,
+rwrt_status rwrt_rk45_run_tv(rwrt_ctx* ctx, const rwrt_grid* g, const rwrt_background* b,
                              int64_t nray, const rwrt_params* p,
                              const double* d_tbound, int32_t it_begin,
                              int32_t it_end, const int64_t* d_order,

@@ -13,7 +13,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("RWRT_LIB", os.path.join(_HERE, "librwrt.so"))
 
 NFIELD_REF, NFIELD_PACK, NVAR, NMERC, NOUT, NSTATE = 18, 12, 5, 12, 8, 12
-ABI_SYMBOLS = ("rwrt_version", "rwrt_last_error", "rwrt_pack_fields",
+ABI_SYMBOLS = ("rwrt_version", "rwrt_last_error", "rwrt_ctx_create", "rwrt_ctx_destroy",
+               "rwrt_pack_fields",
                "rwrt_mercator_point", "rwrt_rhs", "rwrt_dp54_attempt",
                "rwrt_ray_initial", "rwrt_rk45_init", "rwrt_rk45_run", "rwrt_rk4_run",
                "rwrt_bs_ready", "rwrt_rk45_init_tv", "rwrt_rk45_run_tv", "rwrt_rhs_tv",
@@ -74,11 +75,13 @@ def load():
         "rwrt_dp54_attempt": [G, _P, _I64, _P, _P, _P, _D, _D, _P, _P, _P, _P],
         "rwrt_ray_initial": [G, _P, _I64, _P, _P, _P, _I32, _P, _P, _P, _P],
         "rwrt_rk45_init": [G, _P, _I64, _P, Pr, _P, _P, _P, _P, _P, _P],
-        "rwrt_rk45_run": [G, _P, _I64, Pr, _P, _I32, _I32, _P, _I64, _P, _P, _P, _P, _P, _P],
-        "rwrt_rk4_run": [G, _P, _I64, Pr, _I32, _I32, _P, _P, _P, _P, _P, _P, _P],
+        "rwrt_rk45_run": [_P, G, _P, _I64, Pr, _P, _I32, _I32, _P, _I64, _P, _P, _P, _P, _P, _P],
+        "rwrt_rk4_run": [_P, G, _P, _I64, Pr, _I32, _I32, _P, _P, _P, _P, _P, _P, _P],
         "rwrt_bs_ready": [_I32, _I32, _P, _P, _P, _D, _D, _P, _P, _I32, _P],
         "rwrt_rk45_init_tv": [G, B, _I64, _P, Pr, _P, _P, _P, _P, _P, _P],
-        "rwrt_rk45_run_tv": [G, B, _I64, Pr, _P, _I32, _I32, _P, _I64, _P, _P, _P, _P, _P, _P],
+        "rwrt_rk45_run_tv": [_P, G, B, _I64, Pr, _P, _I32, _I32, _P, _I64, _P, _P, _P, _P, _P, _P],
+        "rwrt_ctx_create": [_I32, ctypes.POINTER(_P)],
+        "rwrt_ctx_destroy": [_P],
         "rwrt_rhs_tv": [G, B, _I64, _P, _P, _P, _P],
         "rwrt_kat_rk45": [_I32, _I64, _P, _I32, _P, _D, _D, _D, _P, _P],
         "rwrt_selftest_math": [_I32, _I64, _P, _P, _P, _P],
@@ -120,5 +123,34 @@ def dptr(t, dtype=None, what="tensor"):
     return t.data_ptr()
 
 
-def stream():
-    return torch.cuda.current_stream().cuda_stream
+def stream(device=None):
+    """The current HIP stream of ``device`` (default: torch's current device)."""
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+class Context:
+    """An ``rwrt_ctx`` (include/rwrt.h): the scratch of the ray-loop entry points
+    on one device.  Engines own one each; distinct contexts are independent."""
+
+    def __init__(self, device):
+        require_gpu()
+        self.device = torch.device(device)
+        idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        h = _P()
+        check(load().rwrt_ctx_create(int(idx), ctypes.byref(h)))
+        self._h = h
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        h, self._h = getattr(self, "_h", None), None
+        if h is not None and h.value and _lib is not None:
+            _lib.rwrt_ctx_destroy(h)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:   # interpreter shutdown
+            pass

@@ -18,6 +18,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <string>
 
 #include "rwrt.h"
@@ -1925,8 +1926,10 @@ __global__ void __launch_bounds__(256, RWRT_WAVES_PER_SIMD) rk4_run_kernel(Rk4Ar
 #pragma unroll
         for (int v = 0; v < 5; ++v) y[v] = y[v] + sixth * acc[v];
         nstep += nan_in ? 0 : 1;
-      } else if (!bad1) {
-        ++nhold;
+      } else if (!nan_in) {
+        // held by a masked stage; a masked FIRST stage holds the ray for every
+        // remaining step (its rows repeat to the chunk's end, below), each counted
+        nhold += bad1 ? (a.it_end - it) : 1;
       }
       // post-processing (wr.py:718-756)
       if (fabs(y[1]) >= kHalfPi) {
@@ -2215,29 +2218,14 @@ unsigned grid_for(int64_t n, int block) {
   return (unsigned)b;
 }
 
-int compute_units() {
-  static int cached = 0;
-  if (cached) return cached;
-  int dev = 0, ncu = 0;
-  if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 1)
-    ncu = 256;
-  cached = ncu;
-  return cached;
-}
-
+// Occupancy-derived persistent grid of rk45_run_kernel<BG> on the current device.
 template <class BG = StaticBG>
-int persistent_blocks() {
-  static int cached = 0;
-  if (cached) return cached;
-  int dev = 0, ncu = 0, per = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return 1024;
-  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) ncu = 256;
+int persistent_blocks_on(int ncu) {
+  int per = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
           &per, reinterpret_cast<const void*>(rk45_run_kernel<BG>), 256, 0) != hipSuccess || per < 1)
     per = 1;
-  cached = ncu * per;
-  return cached;
+  return ncu * per;
 }
 
 // solver construction / ray loop launchers shared by the static and the
@@ -2263,49 +2251,108 @@ rwrt_status launch_init(const BG& B, int64_t nray, const double* d_y0, const rwr
 #ifndef RWRT_FROZEN_FILL
 #define RWRT_FROZEN_FILL 1
 #endif
-// Per-device scratch of launch_run: the frozen flags (one byte per ray, grown
-// on demand), the side stream of frozen_fill_kernel and its two events.
-struct FillScratch {
+}  // namespace rwrt
+
+// An execution context (include/rwrt.h rwrt_ctx): everything the ray-loop
+// entry points need beyond the caller's buffers -- the frozen-ray flags (one
+// byte per ray, grown on demand), the side stream the fill kernels run on and
+// its events, and the device's launch geometry.  Distinct contexts share
+// nothing, so calls through them are reentrant and may run concurrently on
+// different streams; one context used from several threads is serialised by
+// its mutex (host bookkeeping only -- the GPU work stays asynchronous), and a
+// call on another stream than the context's previous call waits on the device
+// for that call's end before it rewrites the flags.
+struct rwrt_ctx {
+  int device = 0;
+  int ncu = 256;
+  int blocks_static = 0, blocks_f32 = 0, blocks_f64 = 0;   // persistent grids
   uint8_t* flags = nullptr;
   size_t cap = 0;
   hipStream_t side = nullptr;
   hipEvent_t flagged = nullptr, filled = nullptr;
-  hipEvent_t done = nullptr;   // end of the last call: calls on other streams wait for it
+  hipEvent_t done = nullptr;   // end of the last call on this context
   bool used = false;
+  std::mutex mu;
 };
-FillScratch* fill_scratch(int64_t nray) {
-  static FillScratch cache[64];
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  FillScratch& f = cache[dev];
-  if (!f.side) {
-    if (hipStreamCreateWithFlags(&f.side, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&f.flagged, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&f.filled, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&f.done, hipEventDisableTiming) != hipSuccess) {
-      f.side = nullptr;
-      return nullptr;
-    }
+
+namespace rwrt {
+
+// Makes ctx->device current for the duration of a call (restored after).
+struct DeviceGuard {
+  int prev = -1;
+  bool ok = true;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) ok = hipSetDevice(dev) == hipSuccess;
   }
-  if ((size_t)nray > f.cap) {
-    if (f.flags) {
-      // earlier launches may still read the old flags
-      if (hipDeviceSynchronize() != hipSuccess || hipFree(f.flags) != hipSuccess) return nullptr;
-      f.flags = nullptr;
-      f.cap = 0;
-    }
-    const size_t cap = ((size_t)nray + 4095) & ~(size_t)4095;
-    if (hipMalloc(reinterpret_cast<void**>(&f.flags), cap) != hipSuccess) return nullptr;
-    f.cap = cap;
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
   }
-  return &f;
+};
+
+// Flags for nray rays.  A buffer that earlier calls of this context may still
+// read is freed only after the last of them (its `done` event) has finished.
+rwrt_status ctx_flags(rwrt_ctx* c, int64_t nray) {
+  if ((size_t)nray <= c->cap) return RWRT_OK;
+  if (c->flags) {
+    if ((c->used && hipEventSynchronize(c->done) != hipSuccess) || hipFree(c->flags) != hipSuccess)
+      return check_launch("releasing the context's frozen-ray flags");
+    c->flags = nullptr;
+    c->cap = 0;
+  }
+  const size_t cap = ((size_t)nray + 4095) & ~(size_t)4095;
+  if (hipMalloc(reinterpret_cast<void**>(&c->flags), cap) != hipSuccess)
+    return fail(RWRT_ERR_HIP, "frozen-ray flag allocation failed%s");
+  c->cap = cap;
+  return RWRT_OK;
+}
+
+template <class BG> int& ctx_blocks(rwrt_ctx* c);
+template <> int& ctx_blocks<StaticBG>(rwrt_ctx* c) { return c->blocks_static; }
+template <> int& ctx_blocks<VaryingBG<float>>(rwrt_ctx* c) { return c->blocks_f32; }
+template <> int& ctx_blocks<VaryingBG<double>>(rwrt_ctx* c) { return c->blocks_f64; }
+
+template <class BG>
+int ctx_persistent_blocks(rwrt_ctx* c) {
+  int& b = ctx_blocks<BG>(c);
+  if (!b) b = persistent_blocks_on<BG>(c->ncu);
+  return b;
+}
+
+// flag kernel on `stream`, then the side stream waits for it
+template <class Flag>
+rwrt_status ctx_begin(rwrt_ctx* c, hipStream_t stream, Flag launch_flags) {
+  // the flags belong to this context: a call on another stream must not
+  // overwrite them while the previous call still reads them
+  if (c->used && hipStreamWaitEvent(stream, c->done, 0) != hipSuccess)
+    return check_launch("hipStreamWaitEvent(previous call of the context)");
+  launch_flags();
+  if (rwrt_status s = check_launch("flag kernel")) return s;
+  if (hipEventRecord(c->flagged, stream) != hipSuccess || hipStreamWaitEvent(c->side, c->flagged, 0) != hipSuccess)
+    return check_launch("hipEventRecord(frozen flags)");
+  return RWRT_OK;
+}
+// `stream` waits for the fill on the side stream; the call ends there
+rwrt_status ctx_end(rwrt_ctx* c, hipStream_t stream) {
+  if (hipEventRecord(c->filled, c->side) != hipSuccess || hipStreamWaitEvent(stream, c->filled, 0) != hipSuccess ||
+      hipEventRecord(c->done, stream) != hipSuccess)
+    return check_launch("hipEventRecord(frozen fill)");
+  c->used = true;
+  return RWRT_OK;
+}
+
+rwrt_status ctx_check(rwrt_ctx* c) {
+  if (!c) return fail(RWRT_ERR_ARG, "rwrt_ctx is NULL (create one with rwrt_ctx_create)%s");
+  return RWRT_OK;
 }
 
 template <class BG>
-rwrt_status launch_run(const BG& B, int64_t nray, const rwrt_params* p, const double* d_tbound,
-                       int32_t it_begin, int32_t it_end, const int64_t* d_order, int64_t n_heavy,
-                       double* d_state, int64_t* d_count, int32_t* d_nanrow, double* d_out,
-                       int32_t* d_work, void* stream) {
+rwrt_status launch_run(rwrt_ctx* ctx, const BG& B, int64_t nray, const rwrt_params* p,
+                       const double* d_tbound, int32_t it_begin, int32_t it_end,
+                       const int64_t* d_order, int64_t n_heavy, double* d_state, int64_t* d_count,
+                       int32_t* d_nanrow, double* d_out, int32_t* d_work, void* stream) {
+  if (rwrt_status s = ctx_check(ctx)) return s;
   if (!p) return fail(RWRT_ERR_ARG, "params is NULL%s");
   if (nray < 0 || nray > 0x7fffffffLL) return fail(RWRT_ERR_ARG, "nray out of range%s");
   if (it_begin < 1 || it_end > p->nt || it_begin >= it_end)
@@ -2316,48 +2363,43 @@ rwrt_status launch_run(const BG& B, int64_t nray, const rwrt_params* p, const do
     return fail(RWRT_ERR_ARG, "output rows must be 16-byte aligned%s");
   if (nray == 0) return RWRT_OK;
   if (n_heavy < 0 || n_heavy > nray) return fail(RWRT_ERR_ARG, "n_heavy out of range%s");
-  if (hipMemsetAsync(d_work, 0, 2 * sizeof(int32_t), (hipStream_t)stream) != hipSuccess)
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  DeviceGuard dg(ctx->device);
+  if (!dg.ok) return check_launch("hipSetDevice(context device)");
+  hipStream_t st = (hipStream_t)stream;
+  if (hipMemsetAsync(d_work, 0, 2 * sizeof(int32_t), st) != hipSuccess)
     return check_launch("hipMemsetAsync(queue)");
-  int64_t blocks = persistent_blocks<BG>();
+  int64_t blocks = ctx_persistent_blocks<BG>(ctx);
   const int64_t need = (nray + 255) / 256;
   if (blocks > need) blocks = need;
   // one high-priority block per CU when at least two blocks share each CU
-  const int ncu = compute_units();
+  const int ncu = ctx->ncu;
   const int heavy_blocks = (d_order && n_heavy > 0 && blocks >= 2 * (int64_t)ncu) ? ncu : 0;
   RunArgs<BG> a{B, nray, p->rtol, p->atol, p->min_step, p->cut_off, p->nt, it_begin, it_end,
                 d_tbound, d_order, d_state, d_count, d_nanrow, d_out, d_work,
                 heavy_blocks ? n_heavy : 0, heavy_blocks, haversine_cut(p->cut_off), nullptr};
 #if RWRT_FROZEN_FILL
-  // frozen rays: flagged on `stream`, filled on the side stream while the run
-  // kernel (which skips them) integrates the rest; `stream` then waits for
-  // the fill, so the call stays one stream-ordered operation for the caller
-  FillScratch* fs = fill_scratch(nray);
-  if (!fs) return fail(RWRT_ERR_HIP, "frozen-ray scratch allocation failed%s");
-  a.frozen = fs->flags;
-  // the flags are shared by every call on this device: a call on another
-  // stream must not overwrite them while an earlier call still reads them
-  if (fs->used && hipStreamWaitEvent((hipStream_t)stream, fs->done, 0) != hipSuccess)
-    return check_launch("hipStreamWaitEvent(previous call)");
-  hipLaunchKernelGGL(frozen_flag_kernel, dim3(grid_for(nray, 256)), dim3(256), 0, (hipStream_t)stream,
-                     d_state, nray, fs->flags);
-  if (rwrt_status s = check_launch("frozen_flag_kernel")) return s;
-  if (hipEventRecord(fs->flagged, (hipStream_t)stream) != hipSuccess ||
-      hipStreamWaitEvent(fs->side, fs->flagged, 0) != hipSuccess)
-    return check_launch("hipEventRecord(frozen flags)");
+  // frozen rays: flagged on `stream`, filled on the context's side stream
+  // while the run kernel (which skips them) integrates the rest; `stream` then
+  // waits for the fill, so the call stays one stream-ordered operation
+  if (rwrt_status s = ctx_flags(ctx, nray)) return s;
+  a.frozen = ctx->flags;
+  if (rwrt_status s = ctx_begin(ctx, st, [&] {
+        hipLaunchKernelGGL(frozen_flag_kernel, dim3(grid_for(nray, 256)), dim3(256), 0, st, d_state, nray,
+                           ctx->flags);
+      }))
+    return s;
 #endif
-  hipLaunchKernelGGL(rk45_run_kernel<BG>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(rk45_run_kernel<BG>, dim3((unsigned)blocks), dim3(256), 0, st, a);
   if (rwrt_status s = check_launch("rk45_run_kernel")) return s;
 #if RWRT_FROZEN_FILL
   hipLaunchKernelGGL(frozen_fill_kernel<BG>, dim3((unsigned)((nray + kFillThreads - 1) / kFillThreads)),
-                     dim3(kFillThreads), 0, fs->side, a);
+                     dim3(kFillThreads), 0, ctx->side, a);
   if (rwrt_status s = check_launch("frozen_fill_kernel")) return s;
-  if (hipEventRecord(fs->filled, fs->side) != hipSuccess ||
-      hipStreamWaitEvent((hipStream_t)stream, fs->filled, 0) != hipSuccess ||
-      hipEventRecord(fs->done, (hipStream_t)stream) != hipSuccess)
-    return check_launch("hipEventRecord(frozen fill)");
-  fs->used = true;
-#endif
+  return ctx_end(ctx, st);
+#else
   return RWRT_OK;
+#endif
 }
 
 // a time-varying background from the ABI description
@@ -2507,7 +2549,51 @@ using namespace rwrt;
 
 extern "C" {
 
-const char* rwrt_version(void) { return "rwrt 0.1 (gfx950, abi 1)"; }
+const char* rwrt_version(void) { return "rwrt 0.2 (gfx950, abi 2)"; }
+
+rwrt_status rwrt_ctx_create(int32_t device, rwrt_ctx** out) {
+  if (!out) return fail(RWRT_ERR_ARG, "out is NULL%s");
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
+    return fail(RWRT_ERR_ARG, "no such HIP device%s");
+  DeviceGuard dg(device);
+  if (!dg.ok) return check_launch("hipSetDevice");
+  rwrt_ctx* c = new (std::nothrow) rwrt_ctx;
+  if (!c) return fail(RWRT_ERR_HIP, "out of host memory%s");
+  c->device = device;
+  int ncu = 0;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
+    c->ncu = ncu;
+  if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->flagged, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->filled, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->done, hipEventDisableTiming) != hipSuccess) {
+    rwrt_status s = check_launch("creating the context's stream and events");
+    rwrt_ctx_destroy(c);
+    return s ? s : fail(RWRT_ERR_HIP, "creating the context's stream and events failed%s");
+  }
+  *out = c;
+  return RWRT_OK;
+}
+
+rwrt_status rwrt_ctx_destroy(rwrt_ctx* c) {
+  if (!c) return RWRT_OK;
+  rwrt_status s = RWRT_OK;
+  {
+    std::lock_guard<std::mutex> lock(c->mu);
+    DeviceGuard dg(c->device);
+    // the last call's kernels may still read the flags / run on the side stream
+    if (c->used && hipEventSynchronize(c->done) != hipSuccess) s = check_launch("rwrt_ctx_destroy");
+    if (c->flags) (void)hipFree(c->flags);
+    if (c->side) (void)hipStreamDestroy(c->side);
+    if (c->flagged) (void)hipEventDestroy(c->flagged);
+    if (c->filled) (void)hipEventDestroy(c->filled);
+    if (c->done) (void)hipEventDestroy(c->done);
+  }
+  delete c;
+  return s;
+}
 
 const char* rwrt_last_error(void) { return g_err.c_str(); }
 
@@ -2585,14 +2671,14 @@ rwrt_status rwrt_rk45_init(const rwrt_grid* g, const double* d_packed, int64_t n
                      stream);
 }
 
-rwrt_status rwrt_rk45_run(const rwrt_grid* g, const double* d_packed, int64_t nray,
-                          const rwrt_params* p, const double* d_tbound, int32_t it_begin,
-                          int32_t it_end, const int64_t* d_order, int64_t n_heavy,
-                          double* d_state, int64_t* d_count, int32_t* d_nanrow, double* d_out,
-                          int32_t* d_work, void* stream) {
+rwrt_status rwrt_rk45_run(rwrt_ctx* ctx, const rwrt_grid* g, const double* d_packed,
+                          int64_t nray, const rwrt_params* p, const double* d_tbound,
+                          int32_t it_begin, int32_t it_end, const int64_t* d_order,
+                          int64_t n_heavy, double* d_state, int64_t* d_count, int32_t* d_nanrow,
+                          double* d_out, int32_t* d_work, void* stream) {
   Field F;
   if (rwrt_status s = make_field(g, d_packed, F)) return s;
-  return launch_run(StaticBG{F}, nray, p, d_tbound, it_begin, it_end, d_order, n_heavy, d_state,
+  return launch_run(ctx, StaticBG{F}, nray, p, d_tbound, it_begin, it_end, d_order, n_heavy, d_state,
                     d_count, d_nanrow, d_out, d_work, stream);
 }
 
@@ -2610,20 +2696,20 @@ rwrt_status rwrt_rk45_init_tv(const rwrt_grid* g, const rwrt_background* b, int6
   return launch_init(B, nray, d_y0, p, d_state, d_count, d_nanrow, d_live, d_summary, stream);
 }
 
-rwrt_status rwrt_rk45_run_tv(const rwrt_grid* g, const rwrt_background* b, int64_t nray,
-                             const rwrt_params* p, const double* d_tbound, int32_t it_begin,
+rwrt_status rwrt_rk45_run_tv(rwrt_ctx* ctx, const rwrt_grid* g, const rwrt_background* b,
+                             int64_t nray, const rwrt_params* p, const double* d_tbound, int32_t it_begin,
                              int32_t it_end, const int64_t* d_order, int64_t n_heavy,
                              double* d_state, int64_t* d_count, int32_t* d_nanrow, double* d_out,
                              int32_t* d_work, void* stream) {
   if (b && b->fp32) {
     VaryingBG<float> B;
     if (rwrt_status s = make_varying(g, b, B)) return s;
-    return launch_run(B, nray, p, d_tbound, it_begin, it_end, d_order, n_heavy, d_state, d_count,
+    return launch_run(ctx, B, nray, p, d_tbound, it_begin, it_end, d_order, n_heavy, d_state, d_count,
                       d_nanrow, d_out, d_work, stream);
   }
   VaryingBG<double> B;
   if (rwrt_status s = make_varying(g, b, B)) return s;
-  return launch_run(B, nray, p, d_tbound, it_begin, it_end, d_order, n_heavy, d_state, d_count,
+  return launch_run(ctx, B, nray, p, d_tbound, it_begin, it_end, d_order, n_heavy, d_state, d_count,
                     d_nanrow, d_out, d_work, stream);
 }
 
@@ -2666,11 +2752,12 @@ rwrt_status rwrt_bs_ready(int32_t nlon, int32_t nlat, const float* d_u, const fl
   return check_launch("bs_ready kernels");
 }
 
-rwrt_status rwrt_rk4_run(const rwrt_grid* g, const double* d_packed, int64_t nray,
-                         const rwrt_params* p, int32_t it_begin, int32_t it_end,
+rwrt_status rwrt_rk4_run(rwrt_ctx* ctx, const rwrt_grid* g, const double* d_packed,
+                         int64_t nray, const rwrt_params* p, int32_t it_begin, int32_t it_end,
                          const int64_t* d_order, double* d_state, int64_t* d_count,
                          int32_t* d_nanrow, double* d_out, int32_t* d_work, void* stream) {
   Field F;
+  if (rwrt_status s = ctx_check(ctx)) return s;
   if (rwrt_status s = make_field(g, d_packed, F)) return s;
   if (!p) return fail(RWRT_ERR_ARG, "params is NULL%s");
   if (nray < 0 || nray > 0x7fffffffLL) return fail(RWRT_ERR_ARG, "nray out of range%s");
@@ -2682,41 +2769,38 @@ rwrt_status rwrt_rk4_run(const rwrt_grid* g, const double* d_packed, int64_t nra
   if (reinterpret_cast<uintptr_t>(d_out) % 16 != 0)
     return fail(RWRT_ERR_ARG, "output rows must be 16-byte aligned%s");
   if (nray == 0) return RWRT_OK;
-  if (hipMemsetAsync(d_work, 0, sizeof(int32_t), (hipStream_t)stream) != hipSuccess)
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  DeviceGuard dg(ctx->device);
+  if (!dg.ok) return check_launch("hipSetDevice(context device)");
+  hipStream_t st = (hipStream_t)stream;
+  if (hipMemsetAsync(d_work, 0, sizeof(int32_t), st) != hipSuccess)
     return check_launch("hipMemsetAsync(queue)");
   Rk4Args a{F, nray, p->tstep, p->cut_off, p->nt, it_begin, it_end, d_order, d_state, d_count,
             d_nanrow, d_out, d_work, nullptr};
-  int64_t blocks = persistent_blocks<StaticBG>();
+  int64_t blocks = ctx_persistent_blocks<StaticBG>(ctx);
   const int64_t need = (nray + 255) / 256;
   if (blocks > need) blocks = need;
 #if RWRT_FROZEN_FILL
   // rays whose rows are known at the start go to rk4_fill_kernel on the side
   // stream (as launch_run does for the RK45 loop)
-  FillScratch* fs = fill_scratch(nray);
-  if (!fs) return fail(RWRT_ERR_HIP, "frozen-ray scratch allocation failed%s");
-  a.frozen = fs->flags;
-  if (fs->used && hipStreamWaitEvent((hipStream_t)stream, fs->done, 0) != hipSuccess)
-    return check_launch("hipStreamWaitEvent(previous call)");
-  hipLaunchKernelGGL(rk4_flag_kernel, dim3(grid_for(nray, 256)), dim3(256), 0, (hipStream_t)stream,
-                     d_state, nray, fs->flags);
-  if (rwrt_status s = check_launch("rk4_flag_kernel")) return s;
-  if (hipEventRecord(fs->flagged, (hipStream_t)stream) != hipSuccess ||
-      hipStreamWaitEvent(fs->side, fs->flagged, 0) != hipSuccess)
-    return check_launch("hipEventRecord(rk4 flags)");
+  if (rwrt_status s = ctx_flags(ctx, nray)) return s;
+  a.frozen = ctx->flags;
+  if (rwrt_status s = ctx_begin(ctx, st, [&] {
+        hipLaunchKernelGGL(rk4_flag_kernel, dim3(grid_for(nray, 256)), dim3(256), 0, st, d_state, nray,
+                           ctx->flags);
+      }))
+    return s;
 #endif
-  hipLaunchKernelGGL(rk4_run_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(rk4_run_kernel, dim3((unsigned)blocks), dim3(256), 0, st, a);
   if (rwrt_status s = check_launch("rk4_run_kernel")) return s;
 #if RWRT_FROZEN_FILL
   hipLaunchKernelGGL(rk4_fill_kernel, dim3((unsigned)((nray + kFillThreads - 1) / kFillThreads)),
-                     dim3(kFillThreads), 0, fs->side, a);
+                     dim3(kFillThreads), 0, ctx->side, a);
   if (rwrt_status s = check_launch("rk4_fill_kernel")) return s;
-  if (hipEventRecord(fs->filled, fs->side) != hipSuccess ||
-      hipStreamWaitEvent((hipStream_t)stream, fs->filled, 0) != hipSuccess ||
-      hipEventRecord(fs->done, (hipStream_t)stream) != hipSuccess)
-    return check_launch("hipEventRecord(rk4 fill)");
-  fs->used = true;
-#endif
+  return ctx_end(ctx, st);
+#else
   return RWRT_OK;
+#endif
 }
 
 rwrt_status rwrt_kat_rk45(int32_t kind, int64_t ncol, const double* d_y0, int32_t nt,

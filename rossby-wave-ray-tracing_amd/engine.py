@@ -64,10 +64,28 @@ class RayEngine:
         self.grid = grid_of(lon, lat, f.shape[0])
         self.packed = torch.empty((f.shape[0], f.shape[1], H.NFIELD_PACK), dtype=F64,
                                   device=self.device)
-        H.check(H.load().rwrt_pack_fields(self.grid, H.dptr(f), H.dptr(self.packed), H.stream()))
+        H.check(H.load().rwrt_pack_fields(self.grid, H.dptr(f), H.dptr(self.packed), self._stream()))
         self.work = torch.zeros(4, dtype=torch.int32, device=self.device)
 
     bg = None   # rwrt_background of a time-varying state (None: the reference's static state)
+    _ctx = None
+
+    @property
+    def ctx(self):
+        """This engine's ``rwrt_ctx`` (the ray-loop scratch), created on first use."""
+        if self._ctx is None:
+            self._ctx = H.Context(self.device)
+        return self._ctx
+
+    def _stream(self):
+        """The current stream of the engine's device (not torch's current device)."""
+        return H.stream(self.device)
+
+    def _event_pair(self):
+        s = torch.cuda.current_stream(self.device)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        return e0, e1, s
 
     @classmethod
     def from_bs(cls, bs, device=None):
@@ -110,7 +128,7 @@ class RayEngine:
         t = torch.as_tensor(t, dtype=F64, device=self.device).contiguous()
         out = torch.empty_like(y)
         H.check(H.load().rwrt_rhs_tv(self.grid, ctypes_ref(self.bg), y.shape[1], H.dptr(t),
-                                     H.dptr(y), H.dptr(out), H.stream()))
+                                     H.dptr(y), H.dptr(out), self._stream()))
         return out
 
     # ------------------------------------------------------------------ T0/T1
@@ -121,7 +139,7 @@ class RayEngine:
         n = lon.numel()
         out = torch.empty((H.NMERC, n), dtype=F64, device=self.device)
         H.check(H.load().rwrt_mercator_point(self.grid, H.dptr(self.packed), n, H.dptr(lon),
-                                             H.dptr(lat), H.dptr(out), H.stream()))
+                                             H.dptr(lat), H.dptr(out), self._stream()))
         return out
 
     def rhs(self, y):
@@ -130,7 +148,7 @@ class RayEngine:
         n = y.shape[1]
         out = torch.empty_like(y)
         H.check(H.load().rwrt_rhs(self.grid, H.dptr(self.packed), n, H.dptr(y), H.dptr(out),
-                                  H.stream()))
+                                  self._stream()))
         return out
 
     def attempt(self, y, f, h, rtol=1e-6, atol=1e-6):
@@ -144,7 +162,7 @@ class RayEngine:
         err = torch.empty(n, dtype=F64, device=self.device)
         H.check(H.load().rwrt_dp54_attempt(self.grid, H.dptr(self.packed), n, H.dptr(y),
                                            H.dptr(f), H.dptr(h), rtol, atol, H.dptr(K),
-                                           H.dptr(yn), H.dptr(err), H.stream()))
+                                           H.dptr(yn), H.dptr(err), self._stream()))
         return K, yn, err
 
     # ------------------------------------------------------- initial rays
@@ -183,7 +201,7 @@ class RayEngine:
         packed = self.packed if self.bg is None else self.levels.level0_f64   # the t = 0 state
         H.check(H.load().rwrt_ray_initial(self.grid, H.dptr(packed), ns, H.dptr(src[0]),
                                           H.dptr(src[1]), H.dptr(src[2]), nz, H.dptr(zc),
-                                          H.dptr(rows), H.dptr(info), H.stream()))
+                                          H.dptr(rows), H.dptr(info), self._stream()))
         return rows, info
 
     def initial_rows(self, source_lon, source_lat, zwn, freq, check=True):
@@ -229,7 +247,7 @@ class RayEngine:
             fn, bg = lib.rwrt_rk45_init_tv, ctypes_ref(self.bg)
         H.check(fn(self.grid, bg, nray, H.dptr(y0), ctypes_ref(p), H.dptr(st["state"]),
                    H.dptr(st["count"]), H.dptr(st["nanrow"]), H.dptr(st["live"]),
-                   H.dptr(st["summary"]), H.stream()))
+                   H.dptr(st["summary"]), self._stream()))
         return st
 
     @staticmethod
@@ -263,11 +281,11 @@ class RayEngine:
         else:
             fn, bg = lib.rwrt_rk45_run_tv, ctypes_ref(self.bg)
         H.check(fn(
-            self.grid, bg, st["nray"], ctypes_ref(p), H.dptr(tbound, F64),
+            self.ctx.handle, self.grid, bg, st["nray"], ctypes_ref(p), H.dptr(tbound, F64),
             int(it_begin), int(it_end), H.dptr(order, torch.int64), int(n_heavy),
             H.dptr(st["state"]),
             H.dptr(st["count"]), H.dptr(st["nanrow"]), H.dptr(out, F64), H.dptr(self.work),
-            H.stream()))
+            self._stream()))
 
     def integrate_rk4(self, y0, nt, tstep, cut_off=0.1, chunk=None, sink=None, out=None,
                       cut_rad=None, events=None, group=None):
@@ -275,7 +293,8 @@ class RayEngine:
 
         Same chunked ``sink`` protocol as ``integrate``; the nacc column and
         ``RunResult.nacc`` count RK4 steps taken, ``nrej`` steps held because a
-        stage input was masked (the ray keeps its state, wr.py:609-618).
+        stage input was masked (the ray keeps its state, wr.py:609-618; a masked
+        first stage holds it for every remaining step, each counted).
         """
         if self.bg is not None:
             raise NotImplementedError("the RK4 loop runs on the reference's static basic state")
@@ -297,14 +316,13 @@ class RayEngine:
             flat = bufs[k % len(bufs)].reshape(-1)
             view = flat[: nray * (i1 - i0) * H.NOUT].view(nray, i1 - i0, H.NOUT)
             if events is not None:
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
+                e0, e1, es = self._event_pair()
             H.check(H.load().rwrt_rk4_run(
-                self.grid, H.dptr(self.packed), nray, ctypes_ref(p), int(i0), int(i1),
+                self.ctx.handle, self.grid, H.dptr(self.packed), nray, ctypes_ref(p), int(i0), int(i1),
                 H.dptr(order, torch.int64), H.dptr(st["state"]), H.dptr(st["count"]),
-                H.dptr(st["nanrow"]), H.dptr(view, F64), H.dptr(self.work), H.stream()))
+                H.dptr(st["nanrow"]), H.dptr(view, F64), H.dptr(self.work), self._stream()))
             if events is not None:
-                e1.record()
+                e1.record(es)
                 events.append((e0, e1))
             if sink is not None:
                 sink(i0, i1, view)
@@ -347,10 +365,28 @@ class RayEngine:
             # rkf45.py:423-425: at the first step every live column has a NaN
             # h_abs -> status -1 -> wr.py:886-887 breaks before storing row 1.
             return RunResult(cnt[:, 0], cnt[:, 1], st["nanrow"], True, 1, n_live)
-        order = self.live_first_order(st)
+        return self.advance(st, p, tb, 1, chunk=chunk, sink=sink, out=out, events=events,
+                            group=group, order_policy=order_policy, first_chunk=first_chunk,
+                            n_live=n_live, n_live_local=n_live_local)
+
+    def advance(self, st, p, tb, start, chunk=None, sink=None, out=None, events=None, group=None,
+                order_policy="priority", first_chunk=None, n_live=None, n_live_local=None,
+                prev_work=None):
+        """Rows ``[start, nt)`` of the ray loop for an initialised state ``st``
+        (``init``, or a shard of one: ``take``), in time chunks; the body of
+        ``integrate``.  ``prev_work`` (each ray's attempt count, accepted +
+        rejected, at the start of an earlier launch) orders the first launch
+        longest-first by the attempts since; otherwise live rays go first."""
+        nt = int(p.nt)
+        nray = st["nray"]
+        cnt = st["count"]
+        if n_live_local is None:
+            n_live_local = int((~torch.isnan(st["state"][:5].sum(0))).sum().item())
+        if n_live is None:
+            n_live = n_live_local
         chunk = chunk or (nt - 1)
         bounds = []
-        i0 = 1
+        i0 = start
         # short leading chunks measure the per-ray cost that orders the next one
         lead = [first_chunk] if isinstance(first_chunk, int) else list(first_chunk or [])
         if order_policy in ("cost", "priority"):
@@ -361,9 +397,11 @@ class RayEngine:
         while i0 < nt:
             bounds.append((i0, min(i0 + chunk, nt)))
             i0 = bounds[-1][1]
-        rows_max = max(b - a for a, b in bounds)
-        prev_work = None
+        rows_max = max([b - a for a, b in bounds] or [1])
         bufs = _row_buffers(out, nray, rows_max, self.device)
+        order = None
+        if prev_work is None or order_policy not in ("cost", "priority"):
+            order = self.live_first_order_of(st)
         for k, (i0, i1) in enumerate(bounds):
             flat = bufs[k % len(bufs)].view(-1)
             view = flat[: nray * (i1 - i0) * H.NOUT].view(nray, i1 - i0, H.NOUT)
@@ -374,10 +412,9 @@ class RayEngine:
                     n_heavy = min(self.heavy_lanes(), n_live_local)
             prev_work = cnt.sum(1)
             if events is not None:
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
+                e0, e1, es = self._event_pair()
                 self.run(st, p, tb, i0, i1, view, order, n_heavy)
-                e1.record()
+                e1.record(es)
                 events.append((e0, e1))
             else:
                 self.run(st, p, tb, i0, i1, view, order, n_heavy)
@@ -391,6 +428,18 @@ class RayEngine:
         res = RunResult(cnt[:, 0], cnt[:, 1], st["nanrow"], False, brk, n_live)
         res.bounds = bounds
         return res
+
+    @staticmethod
+    def take(st, idx):
+        """The per-ray state of rays ``idx`` (a device index tensor): a shard."""
+        return dict(state=st["state"][:, idx].contiguous(), count=st["count"][idx].contiguous(),
+                    nanrow=st["nanrow"][idx].contiguous(), nray=int(idx.numel()))
+
+    @staticmethod
+    def live_first_order_of(st):
+        """Live-first queue order from the state itself (NaN mean = frozen)."""
+        dead = torch.isnan(st["state"][:5].sum(0)).to(torch.int8)
+        return torch.sort(dead, stable=True).indices.to(torch.int64).contiguous()
 
 
 def _row_buffers(out, nray, rows_max, device):
@@ -419,7 +468,7 @@ def kat_rk45(kind, y0, t_eval, rtol, atol, min_step, device="cuda"):
     out = torch.empty((ncol, len(t_eval), nv), dtype=F64, device=device)
     H.check(H.load().rwrt_kat_rk45(int(kind), ncol, H.dptr(y0), len(t_eval), H.dptr(te),
                                    float(max(rtol, 100 * np.finfo(np.float64).eps)), float(atol),
-                                   float(min_step), H.dptr(out), H.stream()))
+                                   float(min_step), H.dptr(out), H.stream(y0.device)))
     return out.permute(1, 2, 0)
 
 
@@ -438,5 +487,5 @@ def selftest_math(name, x, y=None, device="cuda"):
     yt = None if y is None else torch.as_tensor(np.asarray(y, np.float64), device=device).contiguous()
     out = torch.empty_like(x)
     H.check(H.load().rwrt_selftest_math(MATH_KINDS[name], x.numel(), H.dptr(x), H.dptr(yt),
-                                        H.dptr(out), H.stream()))
+                                        H.dptr(out), H.stream(x.device)))
     return out.cpu().numpy()

@@ -76,12 +76,12 @@ class Levels:
             raise ValueError(f"u, v must be [{self.nlat}, {self.nlon}]")
         H.check(H.load().rwrt_bs_ready(self.nlon, self.nlat, H.dptr(u), H.dptr(v),
                                        H.dptr(self.trig), self.dx, self.dy, H.dptr(self.scratch),
-                                       self.packed[j].data_ptr(), int(self.fp32), H.stream()))
+                                       self.packed[j].data_ptr(), int(self.fp32), H.stream(self.device)))
         if j == 0 and self.fp32:
             H.check(H.load().rwrt_bs_ready(self.nlon, self.nlat, H.dptr(u), H.dptr(v),
                                            H.dptr(self.trig), self.dx, self.dy,
                                            H.dptr(self.scratch), self.level0_f64.data_ptr(), 0,
-                                           H.stream()))
+                                           H.stream(self.device)))
 
     def background(self):
         """The ``rwrt_background`` description of these levels."""

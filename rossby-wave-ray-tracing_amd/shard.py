@@ -12,7 +12,11 @@ crosses ranks is setup and collection only:
 * ``reduce_summary`` / ``reduce_max`` -- the reference's two global couplings
   (solver failure, rkf45.py:423-425; early exit, wr.py:853-855) evaluated over
   all ranks so that a sharded run equals the single-GPU run exactly;
-* ``gather_rows``     -- per-chunk trajectory rows back to rank 0.
+* ``gather_rows``     -- per-chunk trajectory rows back to rank 0;
+* ``cost_partition`` / ``run_sharded`` -- BASELINE configs[3] (C4): ONE ray set
+  split over the ranks by measured cost (a short probe launch over every ray,
+  then a longest-first snake deal), each rank integrating its shard, the
+  endpoints and step counters gathered to rank 0.
 
 Works with the ``nccl`` (RCCL) backend on device tensors and with ``gloo`` on
 CPU tensors (tests/test_shard.py).
@@ -119,3 +123,103 @@ def gather_rows(local, idx, nray, dst=0, group=None):
     for s, b, ib in zip(sizes, bufs, ibufs):
         out[ib[:s]] = b[:s]
     return out
+
+
+def cost_partition(cost, frozen, rank, world):
+    """Rays of ``rank`` (sorted device index tensor) in a cost-balanced split.
+
+    Live rays are sorted by ``cost`` (descending, stable: the same order on every
+    rank) and dealt in snake order 0, 1, .., w-1, w-1, .., 0, 0, 1, .. so each
+    rank receives heavy, middling and light rays alike; frozen rays (NaN state,
+    rows written by the fill kernel, no integration) are dealt round-robin.
+    Every rank evaluates the same deterministic rule on the same probe counts,
+    so the split needs no communication.
+    """
+    if world == 1:
+        return torch.arange(cost.numel(), device=cost.device)
+    key = torch.where(frozen, torch.full_like(cost, -1), cost)
+    order = torch.sort(key, descending=True, stable=True).indices
+    n_live = int((~frozen).sum().item())
+    pos = torch.arange(order.numel(), device=cost.device)
+    blk, r = pos // world, pos % world
+    owner = torch.where(blk % 2 == 0, r, world - 1 - r)
+    # frozen rays (the tail of ``order``): plain round-robin
+    owner = torch.where(pos >= n_live, (pos - n_live) % world, owner)
+    return torch.sort(order[owner == rank]).values
+
+
+class ShardedRun:
+    """Outcome of ``run_sharded`` on one rank."""
+
+    def __init__(self, idx, res, steps_local, endpoints=None, counts=None, failed=False):
+        self.idx = idx                  # this rank's rays (device index tensor)
+        self.res = res                  # engine.RunResult of the shard (None if failed)
+        self.steps_local = steps_local  # accepted steps of this rank's rays
+        self.endpoints = endpoints      # rank 0: last row [nray, 8] of every ray
+        self.counts = counts            # rank 0: [nray, 2] accepted / rejected
+        self.failed = failed
+
+
+def run_sharded(eng, y0, nt, tstep=7200.0, group=None, rank=None, world=None, probe=6,
+                lead=(24, 96), chunk=None, out=None, sink=None, events=None, gather=True,
+                ttotal=None, order_policy="priority"):
+    """One ray set ``y0[5, nray]`` (identical on every rank) integrated across
+    the ranks of ``group``.
+
+    Every rank constructs the solver for all rays and runs the first ``probe``
+    output rows for all of them (identical, cheap: ~0.5 % of a 90-day run);
+    the attempts each ray needed there decide the split (``cost_partition``).
+    Each rank then integrates only its own rays to ``nt`` and ``gather`` sends
+    their last row and step counters to rank 0 (RCCL ``gather`` on device
+    tensors).  ``sink(i0, i1, rows, idx)`` receives this rank's rows.
+    ``rank``/``world`` without a group emulate one rank of a larger job on
+    this device (single-GPU rehearsal: no collectives).  Rays are independent
+    and both global couplings are decided over every ray, so the union of the
+    shards equals the single-GPU run bit for bit.
+    """
+    from engine import t_eval_of
+    if rank is None:
+        rank, world = world_info(group)
+    p = eng.params(nt, tstep)
+    y0 = torch.as_tensor(y0, dtype=torch.float64, device=eng.device).contiguous()
+    nray = y0.shape[1]
+    tb = torch.as_tensor(t_eval_of(nt, tstep, ttotal), dtype=torch.float64, device=eng.device)
+    st = eng.init(y0, p)
+    summary = st["summary"].cpu()
+    if int(summary[0]) > 0 and int(summary[1]) == 0:      # rkf45.py:423-425 (all rays, every rank)
+        return ShardedRun(None, None, 0, failed=True)
+    npr = min(probe, nt - 1)
+    prow = torch.empty((nray, npr, 8), dtype=torch.float64, device=eng.device)
+    if events is not None:
+        e0, e1, es = eng._event_pair()
+    eng.run(st, p, tb, 1, 1 + npr, prow, eng.live_first_order_of(st), 0)
+    if events is not None:
+        e1.record(es)
+        events.append((e0, e1))
+    cost = st["count"].sum(1)                        # attempts in the probe
+    frozen = torch.isnan(st["state"][:5].sum(0))
+    idx = cost_partition(cost, frozen, rank, world)
+    local = eng.take(st, idx)
+    last = {}
+
+    def keep(i0, i1, rows):
+        last["row"] = rows[:, -1]
+        if sink is not None:
+            sink(i0, i1, rows, idx)
+
+    keep(1, 1 + npr, prow[idx])
+    n_live_local = int((~frozen[idx]).sum().item())
+    res = eng.advance(local, p, tb, 1 + npr, chunk=chunk, sink=keep, out=out, events=events,
+                      group=group, order_policy=order_policy, first_chunk=list(lead),
+                      n_live=int(summary[0]), n_live_local=n_live_local,
+                      prev_work=torch.zeros_like(cost[idx]))
+    steps_local = int(local["count"][:, 0].sum().item())
+    ends = cnts = None
+    if gather:
+        end_row = last["row"].clone()
+        if group is not None and world > 1:
+            ends = gather_rows(end_row, idx.cpu().numpy(), nray, group=group)
+            cnts = gather_rows(local["count"], idx.cpu().numpy(), nray, group=group)
+        elif world == 1:
+            ends, cnts = end_row, local["count"]
+    return ShardedRun(idx, res, steps_local, ends, cnts)

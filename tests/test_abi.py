@@ -38,6 +38,20 @@ def test_argument_errors_are_reported_without_a_gpu():
     assert b"grid" in lib.rwrt_last_error()
     g = H.Grid(145, 73, 0.0, 0.04363323, -1.5707964, 0.04363323)
     p = H.Params(1e-6, 1e-6, 7.2, 0.2, 1081, 0, 7200.0)
-    st = lib.rwrt_rk45_run(ctypes.byref(g), 16, 10, ctypes.byref(p), None, 0, 5, None, 0,
+    st = lib.rwrt_rk45_run(None, ctypes.byref(g), 16, 10, ctypes.byref(p), None, 0, 5, None, 0,
                            None, None, None, None, None, None)
     assert st == H.RWRT_ERR_ARG
+    # the ray loop needs an execution context
+    st = lib.rwrt_rk4_run(None, ctypes.byref(g), 16, 10, ctypes.byref(p), 1, 5, None, None, None,
+                          None, None, None, None)
+    assert st == H.RWRT_ERR_ARG and b"rwrt_ctx" in lib.rwrt_last_error()
+
+
+def test_context_needs_a_device():
+    """rwrt_ctx_create refuses a device that does not exist (none on the build
+    host); destroying NULL is a no-op."""
+    lib = H.load()
+    h = ctypes.c_void_p()
+    assert lib.rwrt_ctx_create(4096, ctypes.byref(h)) == H.RWRT_ERR_ARG
+    assert not h.value
+    assert lib.rwrt_ctx_destroy(None) == H.RWRT_OK

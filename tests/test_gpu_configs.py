@@ -1,0 +1,212 @@
+"""The ray loop on the BASELINE configurations C3, C4 and C5 (BASELINE.json
+configs[2..4]) against the oracle.
+
+* C3 -- the full 2.40 M-slot C3 set integrated 12 days on the GPU; on a
+  cost-stratified sample of 16 384 live rays (tests/golden/c3_sample.npz, made
+  by tools/c3_sample.py: the 512 rays with the most attempts in day 1 plus
+  random rays from 31 cost quantiles) every row must equal the oracle run on
+  the device's transcendentals BIT FOR BIT (all 7 variables, 144 rows,
+  accepted-step counts), and the distance to the NumPy oracle (the reference's
+  own arithmetic) must stay within the tiers of DESIGN.md §2, judged against
+  the reference's own 1-ulp noise floor measured ON THIS SAMPLE
+  (tests/golden/noise_floor_C3_zonal.json).
+* C4 -- the same sample as ONE ray set split over a world-2 group by measured
+  cost (shard.run_sharded: probe launch, snake deal, per-rank integration,
+  gather to rank 0), bit-identical to the 1-GPU run.
+* C5 -- 0.25-degree time-varying background, 4 096 live rays from the C5 seed
+  grid, 2 days through 9 levels, fp64 and fp32 level storage, bit-identical to
+  the oracle's TimeVaryingBackground on the device's transcendentals.
+"""
+import json
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, golden
+
+pytestmark = pytest.mark.gpu
+C3_DAYS = 12
+
+
+def same(a, b):
+    a = np.where(np.isnan(a), np.nan, np.asarray(a, np.float64))
+    b = np.where(np.isnan(b), np.nan, np.asarray(b, np.float64))
+    return np.array_equal(a.view(np.int64), b.view(np.int64))
+
+
+def ndiff(a, b):
+    return int((~((a == b) | (np.isnan(a) & np.isnan(b)))).sum())
+
+
+_C3 = {}
+
+
+def c3_run():
+    """Full C3 on the GPU for C3_DAYS; rows (ray, row, 8) of the sample rays."""
+    if "gpu" not in _C3:
+        import torch
+        from bench import c3_initial_state, c3_sources, make_bs
+        from engine import RayEngine
+        bs, bg = make_bs("zonal")
+        eng = RayEngine.from_bs(bs)
+        src, zcs = c3_sources(eng)
+        y0 = torch.cat([eng.initial_rows_dev(src, zc)[0][:5].reshape(5, -1) for zc in zcs], dim=1)
+        g = golden("c3_sample.npz")
+        assert y0.shape[1] == int(g["nslot"])
+        sel = torch.as_tensor(g["idx"], device=eng.device)
+        nt = C3_DAYS * 12 + 1
+        rows = {}
+        res = eng.integrate(y0, nt, 7200.0, chunk=48, first_chunk=[6, 24],
+                            sink=lambda a, b, o: rows.__setitem__(a, o[sel].cpu().numpy()))
+        hist = np.concatenate([rows[k] for k in sorted(rows)], axis=1)
+        y0h = c3_initial_state(bs)
+        # the GPU initial rows are the host rows (tests/test_gpu_parity.py), here too
+        assert same(y0[:, sel].cpu().numpy(), y0h[:, g["idx"]])
+        _C3["gpu"] = (hist, res.nacc[sel].cpu().numpy(), y0h[:, g["idx"]].copy(), bg, nt)
+    return _C3["gpu"]
+
+
+def test_c3_sample_bitwise_with_device_math():
+    import rwrt_oracle as O
+    hist, nacc, y0, bg, nt = c3_run()
+    with np.errstate(all="ignore"), O.device_math():
+        ref, rnacc, _, st = O.ray_run(O.Background(**bg), y0.copy(), nt, 7200.0)
+    assert st == 0
+    g = np.transpose(hist[:, :, :7], (2, 1, 0))
+    assert same(g, ref[:, 1:]), f"{ndiff(g, ref[:, 1:])} values differ"
+    assert np.array_equal(nacc, rnacc)
+    # the nacc column of every row is the running accepted-step count
+    assert np.array_equal(hist[:, -1, 7].astype(np.int64), rnacc)
+
+
+def test_c3_sample_vs_reference_arithmetic():
+    """Distance to the NumPy oracle (bit-exact with the reference) per horizon,
+    against the reference's own spread under a 1-ulp RHS perturbation."""
+    import rwrt_oracle as O
+    hist, nacc, y0, bg, nt = c3_run()
+    floor = json.load(open(os.path.join(GOLDEN, "noise_floor_C3_zonal.json")))
+    with np.errstate(all="ignore"):
+        ref, rnacc, _, st = O.ray_run(O.Background(**bg), y0.copy(), nt, 7200.0)
+    report = {}
+    for row, key in ((1, "0.0833333d"), (12, "1d"), (48, "4d"), (nt - 1, f"{(nt - 1) / 12:g}d")):
+        a, b = hist[:, row - 1, :2], ref[:2, row].T
+        flips = int(np.sum(np.isnan(a[:, 0]) != np.isnan(b[:, 0])))
+        ok = ~np.isnan(a).any(1) & ~np.isnan(b).any(1)
+        d = np.max(np.abs(a[ok] - b[ok]), axis=1)
+        f = floor[key]
+        report[key] = (float(np.percentile(d, 99)), float(d.max()), flips)
+        if row == 1:   # T2: every ray within the north-star tolerance after one step interval
+            assert d.max() <= 1e-6 and flips == 0, report
+        else:          # T2/T3: within 3x the reference's own spread on this sample
+            assert np.percentile(d, 99) <= max(3 * f["p99"], 1e-12), report
+            assert d.max() <= max(3 * f["max"], 1e-12), report
+            assert flips <= max(3 * f["alive_flips"], len(d) // 1000), report
+    print("C3 sample vs reference arithmetic (p99, max, alive flips):", report)
+
+
+# ---------------------------------------------------------------- C4
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _c4_worker(rank, world, port, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    sys.path[:0] = [os.path.join(root, "rossby-wave-ray-tracing_amd"), root, here]
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from bench import c3_initial_state, make_bs
+        from engine import RayEngine
+        from shard import broadcast_array, gather_rows, run_sharded
+        bs, bg = make_bs("zonal")
+        # rank 0's basic state is the one every rank integrates through
+        fields = broadcast_array(bs.fields if rank == 0 else None)
+        eng = RayEngine(fields, bs.lon, bs.lat)
+        g = np.load(os.path.join(here, "golden", "c3_sample.npz"))
+        y0 = c3_initial_state(bs)[:, g["idx"]]
+        nt = C3_DAYS * 12 + 1
+        parts = []
+        r = run_sharded(eng, y0, nt, group=dist.group.WORLD, chunk=48,
+                        sink=lambda a, b, o, idx: parts.append(o.cpu()))
+        mine = torch.cat(parts, dim=1)                      # (n_local, nt-1, 8)
+        full = gather_rows(mine, r.idx.cpu().numpy(), y0.shape[1], group=dist.group.WORLD)
+        if rank == 0:
+            q.put(("ok", full.numpy(), r.counts.cpu().numpy(), r.endpoints.cpu().numpy(),
+                   int(r.idx.numel())))
+        else:
+            q.put(("rank1", int(r.idx.numel())))
+    except Exception as e:  # pragma: no cover
+        q.put(("err", repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_c4_cost_sharded_world2_equals_single_gpu():
+    import torch.multiprocessing as mp
+    hist, nacc, y0, bg, nt = c3_run()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_c4_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    msgs = [q.get(timeout=110) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+    ok = [m for m in msgs if m[0] == "ok"]
+    assert ok, msgs
+    _, full, counts, ends, n0 = ok[0]
+    n1 = [m for m in msgs if m[0] == "rank1"][0][1]
+    assert n0 + n1 == hist.shape[0] and abs(n0 - n1) <= 2     # balanced, disjoint, complete
+    assert same(full[:, :, :7], hist[:, :, :7])
+    assert np.array_equal(counts[:, 0], nacc)
+    assert same(ends, hist[:, -1])
+
+
+# ---------------------------------------------------------------- C5
+@pytest.mark.parametrize("fp32", [False, True])
+def test_c5_025deg_bitwise_with_device_math(fp32):
+    import torch
+    import rwrt_oracle as O
+    import synthetic as S
+    from engine import RayEngine
+    from levels import Levels
+    dt, nlev, nt = 6 * 3600.0, 9, 25          # 2 days at 2 h through 9 six-hourly levels
+    bl = [S.background_level(j, res=0.25) for j in range(nlev)]
+    lv = Levels(bl[0]["lat"], bl[0]["lon"], nlev, t0=0.0, dt=dt, fp32=fp32)
+    for j, b in enumerate(bl):
+        lv.set_level(j, b["u"], b["v"])
+    eng = RayEngine.from_levels(lv)
+    cfg = S.config("C5")
+    slon, slat = O.source_matrix(cfg.SW_lon, cfg.SW_lat, cfg.dlon, cfg.dlat, cfg.nnx, cfg.nny)
+    rows = eng.initial_rows(slon, slat, cfg.zwn, S.c3_freq(S.C5_PERIODS_DAYS[-1])).cpu().numpy()
+    y0 = rows[:5].reshape(5, -1)
+    live = np.where(~np.isnan(y0.mean(axis=0)))[0]
+    pick = np.sort(np.random.default_rng(3).choice(live, size=4096, replace=False))
+    y0 = y0[:, pick].copy()
+    got = {}
+    res = eng.integrate(torch.as_tensor(y0), nt, 7200.0, ttotal=(nt - 1) * 7200.0, chunk=12,
+                        sink=lambda a, b, o: got.__setitem__(a, o.cpu().numpy().copy()))
+    hist = np.concatenate([got[k] for k in sorted(got)], axis=1)
+    del eng, lv
+    torch.cuda.empty_cache()
+    ob = O.TimeVaryingBackground([O.Background(**b) for b in bl], 0.0, dt, fp32=fp32)
+    with np.errstate(all="ignore"), O.device_math():
+        ref, nacc, _, st = O.ray_run(ob, y0.copy(), nt, 7200.0)
+    assert st == 0
+    g = np.transpose(hist[:, :, :7], (2, 1, 0))
+    assert same(g, ref[:, 1:]), f"{ndiff(g, ref[:, 1:])} values differ"
+    assert np.array_equal(res.nacc.cpu().numpy(), nacc)
+    # the sample moves through the levels (not a static-state test in disguise)
+    assert np.nanmax(np.abs(hist[:, -1, 0] - y0[0])) > 0.05

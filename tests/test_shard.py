@@ -82,3 +82,27 @@ def test_world2_gloo_pipeline_equals_unsharded():
     assert np.array_equal(full, ref, equal_nan=True)
     assert summ == [nlive, 1]
     assert mx == 11
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_cost_partition_is_a_balanced_split(world):
+    """C4's split (shard.cost_partition): disjoint and complete; every rank gets
+    the same number of live rays (+-1) and nearly the same total cost; the
+    heaviest rays spread over the ranks."""
+    import shard
+    rng = np.random.default_rng(2)
+    n = 100_003
+    cost = torch.as_tensor(np.round(rng.lognormal(3.0, 0.8, n)).astype(np.int64))
+    frozen = torch.as_tensor(rng.random(n) < 0.7)
+    parts = [shard.cost_partition(cost, frozen, r, world) for r in range(world)]
+    allidx = torch.sort(torch.cat(parts)).values
+    assert torch.equal(allidx, torch.arange(n))
+    live_n = [int((~frozen[p]).sum()) for p in parts]
+    tot = [int(cost[p][~frozen[p]].sum()) for p in parts]
+    assert max(live_n) - min(live_n) <= 1
+    assert max(tot) - min(tot) <= int(cost.max())          # within one ray's cost
+    top = torch.sort(torch.where(frozen, -1, cost), descending=True).indices[:world]
+    owners = {r for r, p in enumerate(parts) for i in top.tolist() if i in set(p.tolist())}
+    assert len(owners) == world
+    # the same rule on every rank: repeated evaluation is identical
+    assert all(torch.equal(shard.cost_partition(cost, frozen, r, world), parts[r]) for r in range(world))

@@ -1,0 +1,82 @@
+"""C4 on one MI355X: every rank's shard of the cost-balanced split, timed alone.
+
+    python tools/c4_rehearsal.py [--days 90] [--worlds 1,2,4,8] [--out f.json]
+
+For each world size W the C3 set is split exactly as ``bench.py --gpus W``
+splits it (shard.run_sharded: probe launch over every ray, snake deal by probe
+cost); each rank's integration is then run alone on this GPU (no collectives).
+The slowest rank's time is the W-GPU makespan of the ray loop without the
+RCCL broadcast and gather (which bench.py times: ~1 MB and ~55 MB).  Also
+times the single heaviest ray alone -- the critical path no split can beat.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "rossby-wave-ray-tracing_amd")]
+import torch  # noqa: E402
+import bench  # noqa: E402
+from engine import RayEngine  # noqa: E402
+from shard import run_sharded  # noqa: E402
+
+
+def timed(fn, reps=2):
+    fn()
+    torch.cuda.synchronize()
+    best = None
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        r = fn()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        best = dt if best is None else min(best, dt)
+    return best, r
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--days", type=float, default=90)
+    ap.add_argument("--worlds", default="1,2,4,8")
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    bs, bg = bench.make_bs("zonal")
+    y0 = torch.as_tensor(bench.c3_initial_state(bs), device="cuda")
+    eng = RayEngine.from_bs(bs)
+    nt = int(a.days * 12) + 1
+    out = {"days": a.days, "worlds": {}}
+    for w in [int(x) for x in a.worlds.split(",")]:
+        ranks = []
+        for r in range(w):
+            dt, res = timed(lambda: run_sharded(eng, y0, nt, rank=r, world=w, gather=False))
+            ranks.append({"rank": r, "s": dt, "rays": int(res.idx.numel()), "ray_steps": res.steps_local,
+                          "max_attempts": int((res.res.nacc + res.res.nrej).max().item())})
+        steps = sum(x["ray_steps"] for x in ranks)
+        mk = max(x["s"] for x in ranks)
+        out["worlds"][str(w)] = {"makespan_s": mk, "rate": steps / mk, "ray_steps": steps, "ranks": ranks}
+        print(json.dumps({"world": w, "makespan_s": mk, "rate": steps / mk}), flush=True)
+    # the heaviest ray alone (its attempts from the 1-rank run)
+    full = run_sharded(eng, y0, nt, rank=0, world=1, gather=False)
+    work = (full.res.nacc + full.res.nrej)
+    j = int(torch.argmax(work).item())
+    one = y0[:, full.idx[j]:full.idx[j] + 1].contiguous()
+    dt, r1 = timed(lambda: eng.integrate(one, nt, 7200.0, ttotal=(nt - 1) * 7200.0))
+    att = int((r1.nacc + r1.nrej).sum().item())
+    out["heaviest_ray"] = {"slot": int(full.idx[j].item()), "attempts": att, "s": dt,
+                           "us_per_attempt": 1e6 * dt / max(att, 1)}
+    one1 = out["worlds"].get("1")
+    if one1:
+        for k, v in out["worlds"].items():
+            v["speedup_vs_1"] = one1["makespan_s"] / v["makespan_s"]
+    js = json.dumps(out)
+    print(js)
+    if a.out:
+        open(a.out, "w").write(js + "\n")
+
+
+if __name__ == "__main__":
+    main()

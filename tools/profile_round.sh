@@ -11,8 +11,9 @@ B="python3 bench.py --steps 2 --warmup 1 --no-cpu $*"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/trace -o run --output-format csv -- $B > $out/trace.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $out/fetch -o run --output-format csv -- $B > $out/fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $out/write -o run --output-format csv -- $B > $out/write.log 2>&1
-timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU --kernel-trace -d $out/sq -o run --output-format csv -- $B > $out/sq.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY GRBM_GUI_ACTIVE --kernel-trace -d $out/valu -o run --output-format csv -- $B > $out/valu.log 2>&1
 cp $out/trace/run_kernel_stats.csv $sum/kernel_stats.csv
 python3 tools/pmc_traffic.py $out/fetch $out/write $out/trace.log $sum/traffic.json
-cp $out/sq/run_counter_collection.csv $sum/sq_counters.csv
+python3 tools/pmc_valu.py $out/valu $out/trace.log $sum/valu.json
+cp $out/valu/run_counter_collection.csv $sum/valu_counters.csv
 grep -h '^{' $out/trace.log > $sum/bench_under_rocprof.json || true
