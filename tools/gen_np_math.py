@@ -1,0 +1,156 @@
+"""Generate rossby-wave-ray-tracing_amd/csrc/np_math_tables.h: the constants and
+tables of the transcendental routines the reference's NumPy computes with on
+an AVX-512 x86-64 host (tools/host_libm_probe.py shows the
+GPU box's host computes with the same ones):
+
+* ``np.sin``/``np.cos``  -> glibc 2.35 ``__sin_fma``/``__cos_fma`` (the IBM
+  Accurate Mathematical Library's s_sin.c built with FMA): the Taylor and
+  table constants and ``__sincostab`` (110 x {sin, sin tail, cos, cos tail}
+  of k/128);
+* ``np.tan``             -> NumPy 2.2.6's SVML ``__svml_tan8_ha``: pi/16
+  reduction constants, tan(j pi/16) head/tail tables, polynomial;
+* ``np.power``           -> SVML ``__svml_pow8_ha``: log2 / exp2 tables and
+  polynomials;
+* ``VRCP14PD``           -> the host CPU's 14-bit reciprocal approximation
+  that both SVML routines start from: the result depends on the top 16
+  fraction bits of the input only (checked here), stored as 2-bit deltas of
+  consecutive 16-bit result mantissas.
+
+The values are read from the shared objects themselves (file offset ==
+virtual address for their read-only segments) at the addresses their
+machine code loads them from; csrc/np_math.h restates the instruction
+sequences.  Run only in the build container (needs the same libm / numpy and
+an AVX-512 CPU); the generated header is committed.
+
+    python tools/gen_np_math.py
+"""
+import hashlib
+import os
+import struct
+import subprocess
+import tempfile
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = os.path.join(ROOT, "rossby-wave-ray-tracing_amd", "csrc", "np_math_tables.h")
+LIBM = "/lib/x86_64-linux-gnu/libm.so.6"
+
+
+def numpy_so():
+    import numpy._core._multiarray_umath as m
+    return m.__file__
+
+
+def u64(path, addr, n=1):
+    with open(path, "rb") as f:
+        f.seek(addr)
+        b = f.read(8 * n)
+    return list(struct.unpack(f"<{n}Q", b))
+
+
+def sym(path, name):
+    out = subprocess.run(["nm", path], capture_output=True, text=True, check=True).stdout
+    for line in out.splitlines():
+        p = line.split()
+        if len(p) == 3 and p[2] == name:
+            return int(p[0], 16)
+    raise KeyError(name)
+
+
+def hexd(u):
+    return f"0x{u:016X}ull"
+
+
+def rcp14_table():
+    src = os.path.join(ROOT, "tools", "rcp14_probe.c")
+    with tempfile.TemporaryDirectory() as d:
+        exe, out = os.path.join(d, "p"), os.path.join(d, "t.bin")
+        subprocess.run(["gcc", "-O2", "-mavx512f", src, "-o", exe], check=True)
+        subprocess.run([exe, out], check=True)
+        both = np.fromfile(out, dtype=np.uint64)
+    t, t0 = both[:65536], both[65536:]                     # 1 + i/65536 + 2^-52, 1 + i/65536
+    assert t0[0] == 0x3FF0000000000000                     # rcp14(1) = 1 exactly
+    assert np.array_equal(t[1:], t0[1:])                   # only the top 16 fraction bits count
+    assert np.all((t >> np.uint64(52)) == 0x3FE)           # (0.5, 1) otherwise
+    assert np.all((t & np.uint64((1 << 36) - 1)) == 0)     # 16 fraction bits
+    f = ((t >> np.uint64(36)) & np.uint64(0xFFFF)).astype(np.int64)
+    d = f[:-1] - f[1:]                                     # deltas from entry 0 on
+    assert d.min() >= 0 and d.max() <= 3
+    return int(f[0]), d, hashlib.sha256(both.tobytes()).hexdigest()
+
+
+def main():
+    L = {}
+    # glibc 2.35 libm.so.6: addresses the __sin_fma / __cos_fma code loads
+    for name, addr in [("HP0", 0x93048), ("HP1", 0x930B8), ("MHP1", 0x9A870), ("T126", 0x9A878),
+                       ("S5", 0x9A880), ("S4", 0x9A888), ("S3", 0xC1598), ("S2", 0x9A898),
+                       ("S1", 0xC15A0), ("BIG", 0x9A8A8), ("SN5", 0x9A8B0), ("SN3", 0xC15A8),
+                       ("CS6", 0x9A8C0), ("CS4", 0xC15B0), ("CS2", 0x8AAB0), ("TOINT", 0x97010),
+                       ("HPINV", 0x969B8), ("MP1", 0x9A8D0), ("MP2", 0x9A8D8), ("PP3", 0x9A8E0),
+                       ("PP4", 0x9A8E8)]:
+        L[name] = u64(LIBM, addr)[0]
+    tab = u64(LIBM, 0xAEB80, 440)
+    npso = numpy_so()
+    tb = sym(npso, "__svml_dtan_ha_data_internal")
+    pb = sym(npso, "__svml_dpow_ha_data_internal_avx512")
+
+    def bc(base, off):
+        v = u64(npso, base + off, 8)
+        assert all(x == v[0] for x in v), hex(off)
+        return v[0]
+    T = {n: bc(tb, o) for n, o in [("INVPI16", 0x0), ("PI16A", 0x40), ("PI16B", 0x100), ("PI16C", 0x140),
+                                   ("C1", 0x280), ("C2", 0x2C0), ("C3", 0x300), ("C4", 0x340),
+                                   ("C5", 0x380), ("ONE", 0x3C0), ("SHIFT", 0x480), ("BIGARG", 0x6E00)]}
+    tan_hi = u64(npso, tb + 0x180, 16)
+    tan_lo = u64(npso, tb + 0x200, 16)
+    P = {n: bc(pb, o) for n, o in [("HALF", 0x300), ("C1", 0x3C0), ("C10", 0x400), ("C9", 0x440),
+                                   ("C8", 0x480), ("C7", 0x4C0), ("C6", 0x500), ("C5", 0x540),
+                                   ("C4", 0x580), ("C3", 0x5C0), ("LN", 0x600), ("LP", 0x640),
+                                   ("E7", 0x700), ("E6", 0x740), ("E4", 0x780), ("E3", 0x7C0),
+                                   ("E2", 0x800), ("E1", 0x840), ("TOVF", 0x980)]}
+    log_hi = u64(npso, pb + 0x0, 32)
+    log_lo = u64(npso, pb + 0x100, 32)
+    exp_hi = u64(npso, pb + 0x200, 16)
+    exp_lo = u64(npso, pb + 0x280, 16)
+    f1, deltas, sha = rcp14_table()
+    packed = np.zeros((len(deltas) + 15) // 16, np.uint32)
+    for i, d in enumerate(deltas):
+        packed[i // 16] |= np.uint32(int(d) << (2 * (i % 16)))
+
+    lines = ["// GENERATED by tools/gen_np_math.py -- do not edit.",
+             "// Constants and tables of the reference NumPy's transcendentals (see np_math.h):",
+             f"//   glibc: {LIBM} (__sin_fma / __cos_fma, sincostab at 0xaeb80)",
+             f"//   numpy: {os.path.basename(npso)} (numpy {np.__version__}): __svml_tan8_ha, __svml_pow8_ha",
+             f"//   VRCP14PD of this host, sha256 of the 2 x 65536 x f64 probes (tools/rcp14_probe.c) {sha}",
+             "#pragma once", "", "namespace np_math {", ""]
+    for k, v in L.items():
+        lines.append(f"NM_CONST unsigned long long kG_{k} = {hexd(v)};")
+    lines.append("")
+    for k, v in T.items():
+        lines.append(f"NM_CONST unsigned long long kT_{k} = {hexd(v)};")
+    for k, v in P.items():
+        lines.append(f"NM_CONST unsigned long long kP_{k} = {hexd(v)};")
+    lines.append("")
+
+    def arr(name, vals, typ="unsigned long long", per=4, fmt=hexd):
+        lines.append(f"NM_TABLE {typ} {name}[{len(vals)}] = {{")
+        for i in range(0, len(vals), per):
+            lines.append("    " + ", ".join(fmt(int(x)) for x in vals[i:i + per]) + ",")
+        lines.append("};")
+    arr("kG_SINCOSTAB", tab)
+    arr("kT_TAN_HI", tan_hi)
+    arr("kT_TAN_LO", tan_lo)
+    arr("kP_LOG_HI", log_hi)
+    arr("kP_LOG_LO", log_lo)
+    arr("kP_EXP_HI", exp_hi)
+    arr("kP_EXP_LO", exp_lo)
+    lines.append(f"NM_CONST unsigned kRCP14_F0 = {f1}u;   // 16-bit result fraction of entry 0")
+    arr("kRCP14_DELTA", packed, "unsigned", 8, lambda x: f"0x{x:08X}u")
+    lines += ["", "}  // namespace np_math", ""]
+    open(OUT, "w").write("\n".join(lines))
+    print("wrote", OUT, f"({len(deltas)} rcp14 deltas, sha {sha[:16]})")
+
+
+if __name__ == "__main__":
+    main()

@@ -39,12 +39,14 @@ def main():
             bench = json.loads(line)
     n = min(len(f), len(w))
     fb, wb = sum(f[:n]) / n, sum(w[:n]) / n
-    steps_per_launch = bench["ray_steps_per_step"] / (bench["roofline"]["launches"] / bench["steps"])
+    launches_per_step = len(bench["config"]["launch_rows"])
+    steps_per_launch = bench["ray_steps_per_step"] / launches_per_step
+    bps = bench["roofline"].get("bytes_per_ray_step") or bench["roofline"]["algorithmic"]["bytes_per_ray_step"]
     res = {"workload": bench["config"]["workload"], "launch_rows": bench["config"].get("launch_rows"),
            "kernel": "rk45_run_kernel", "kernels_summed": list(KERNELS), "launches": n,
            "fetch_bytes_per_launch_x2": 2 * fb, "write_bytes_per_launch": wb,
            "traffic_bytes_per_launch": 2 * fb + wb,
-           "algorithmic_bytes_per_launch": steps_per_launch * bench["roofline"]["bytes_per_ray_step"],
+           "algorithmic_bytes_per_launch": steps_per_launch * bps,
            "note": "FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE; counters in KiB x 1024"}
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res))
