@@ -59,9 +59,10 @@ ERR_EXP = -1 / (4 + 1)        # rkf45.py:360, error_estimator_order = 4
 # ----------------------------------------------------------------------------
 # transcendentals of the ray loop: NumPy's (glibc sin/cos, SVML tan/power on
 # AVX-512 hosts -- what the reference computes with) by default;
-# ``device_math()`` swaps in the GPU's own (oracle/devmath.cpp, the kernel's
-# rwrt_math.h compiled for the host) so that the oracle and the GPU differ in
-# nothing and whole trajectories compare bit for bit.
+# ``device_math()`` swaps in the GPU kernel's own restatement of them
+# (oracle/npmath.cpp: the kernel's csrc/np_math.h compiled for the host,
+# bitwise equal to NumPy's: tests/test_np_math.py), so that the oracle
+# computes with exactly the kernel's functions on any AVX-512 host.
 # ----------------------------------------------------------------------------
 class _LibM:
     sin = staticmethod(np.sin)
@@ -79,14 +80,14 @@ def _devmath_lib():
     if _DEVMATH is None:
         import ctypes
         import os
-        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_devmath", "libdevmath.so")
+        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_devmath", "libnpmath.so")
         if not os.path.exists(path):
             raise RuntimeError(f"{path} missing: build it with `make -C oracle`")
         lib = ctypes.CDLL(path)
         P, I = ctypes.c_void_p, ctypes.c_int64
-        for name in ("dm_sin", "dm_cos", "dm_tan", "dm_exp"):
+        for name in ("nm_sin_arr", "nm_cos_arr", "nm_tan_arr", "nm_rcp14_arr"):
             getattr(lib, name).argtypes = [P, P, I]
-        lib.dm_pow.argtypes = [P, P, I, P, I]
+        lib.nm_pow_arr.argtypes = [P, P, I, P, I]
         _DEVMATH = lib
     return _DEVMATH
 
@@ -105,17 +106,18 @@ def _dm_power(x, y):
     x, y = np.broadcast_arrays(np.asarray(x, np.float64), np.asarray(y, np.float64))
     xc, yc = np.ascontiguousarray(x), np.ascontiguousarray(y)
     out = np.empty(xc.shape)
-    _devmath_lib().dm_pow(xc.ctypes.data, yc.ctypes.data, 1, out.ctypes.data, xc.size)
+    _devmath_lib().nm_pow_arr(xc.ctypes.data, yc.ctypes.data, 1, out.ctypes.data, xc.size)
     return out
 
 
 class device_math:
-    """Context manager: the oracle uses the GPU's sin/cos/tan/power inside."""
+    """Context manager: the oracle uses the kernel's sin/cos/tan/power inside."""
 
     def __enter__(self):
         _devmath_lib()
         self._saved = (LIBM.sin, LIBM.cos, LIBM.tan, LIBM.power)
-        LIBM.sin, LIBM.cos, LIBM.tan = _dm_unary("dm_sin"), _dm_unary("dm_cos"), _dm_unary("dm_tan")
+        LIBM.sin, LIBM.cos = _dm_unary("nm_sin_arr"), _dm_unary("nm_cos_arr")
+        LIBM.tan = _dm_unary("nm_tan_arr")
         LIBM.power = _dm_power
         return LIBM
 

@@ -880,6 +880,97 @@ __device__ __forceinline__ void sincostan(double x, double& sn, double& cs, doub
   }
   rwrt_math::rm_sincostan_small(x, sn, cs, tn);
 }
+}  // namespace rwrt
+
+// ---------------------------------------------------------------------------
+// The reference NumPy's own transcendentals (np_math.h: glibc 2.35
+// __sin_fma/__cos_fma, SVML __svml_tan8_ha/__svml_pow8_ha), bitwise equal to
+// np.sin/np.cos/np.tan/np.power on the reference's AVX-512 hosts
+// (tests/test_np_math.py on the host, tests/test_gpu_np_math.py here).
+// SVML pow's round-toward-zero / -infinity steps set the f64 round mode for
+// one instruction each (ocml's rounded operations: s_setreg of MODE.FP_ROUND).
+// ---------------------------------------------------------------------------
+extern "C" __device__ double __ocml_fma_rtz_f64(double, double, double);
+extern "C" __device__ double __ocml_mul_rtz_f64(double, double);
+extern "C" __device__ double __ocml_add_rtz_f64(double, double);
+extern "C" __device__ double __ocml_add_rtn_f64(double, double);
+#define NM_FN __device__ __forceinline__
+#define NM_CONST constexpr
+#define NM_TABLE constexpr
+#define NM_FMA_RZ(a, b, c) __ocml_fma_rtz_f64((a), (b), (c))
+#define NM_MUL_RZ(a, b) __ocml_mul_rtz_f64((a), (b))
+#define NM_ADD_RZ(a, b) __ocml_add_rtz_f64((a), (b))
+#define NM_ADD_RD(a, b) __ocml_add_rtn_f64((a), (b))
+#define NM_RCP14_TAB ::np_math::g_nm_rcp14.v
+#define NM_FALLBACK_SIN(x) ::sin(x)
+#define NM_FALLBACK_COS(x) ::cos(x)
+#define NM_FALLBACK_TAN(x) ::tan(x)
+#define NM_FALLBACK_POW(x, y) ::pow((x), (y))
+namespace np_math {
+struct NmRcp14;
+extern __device__ const NmRcp14 g_nm_rcp14;
+}
+#include "np_math.h"
+namespace np_math {
+// VRCP14PD's 64 K-entry result table (128 KB), expanded at compile time
+__device__ const NmRcp14 g_nm_rcp14 = nm_rcp14_table();
+}
+
+namespace rwrt {
+// The kernels' transcendentals: the reference NumPy's (default) or, in the
+// RWRT_MATH_NUMPY=0 diagnostic build, the device library's algorithms
+// (rwrt_math.h; last-bit different from the reference).
+#ifndef RWRT_MATH_NUMPY
+#define RWRT_MATH_NUMPY 1
+#endif
+__device__ __forceinline__ double k_sin(double x) {
+#if RWRT_MATH_NUMPY
+  return np_math::nm_sin(x);
+#else
+  double s, c, t;
+  sincostan(x, s, c, t);
+  return s;
+#endif
+}
+__device__ __forceinline__ double k_cos(double x) {
+#if RWRT_MATH_NUMPY
+  return np_math::nm_cos(x);
+#else
+  double s, c, t;
+  sincostan(x, s, c, t);
+  return c;
+#endif
+}
+__device__ __forceinline__ double k_tan(double x) {
+#if RWRT_MATH_NUMPY
+  return np_math::nm_tan(x);
+#else
+  double s, c, t;
+  sincostan(x, s, c, t);
+  return t;
+#endif
+}
+__device__ __forceinline__ double k_pow(double x, double y) {
+#if RWRT_MATH_NUMPY
+  return np_math::nm_pow(x, y);
+#else
+  return rm_pow(x, y);
+#endif
+}
+// sin, cos, tan of a latitude (the RHS): the same values as k_sin/k_cos/k_tan
+__device__ __forceinline__ void k_sincostan(double x, double& s, double& c, double& t) {
+#if RWRT_MATH_NUMPY
+  s = np_math::nm_sin(x);
+  c = np_math::nm_cos(x);
+  t = np_math::nm_tan(x);
+#elif RWRT_RHS_TRIG_SMALL
+  // |lat| >= 2^30, inf or NaN: the ray is masked (|lat| >= pi/2) or its
+  // lookup is NaN, so every output is NaN whatever s, c, tn are
+  rwrt_math::rm_sincostan_small(x, s, c, t);
+#else
+  sincostan(x, s, c, t);
+#endif
+}
 
 // Mercator factors of cal_bs_mercator_point (bs.py:856-860).
 struct Merc {
@@ -976,20 +1067,8 @@ __device__ __forceinline__ void ray_rhs(const BG& B, double t, const double* y, 
   c = 1.0 - lat * lat * 0.5;
   const double tn = lat * (1.0 + lat * lat * (1.0 / 3.0));
 #else
-#if RWRT_OCML_TRIG
-  sincos(lat, &s, &c);              // one argument reduction for both (== sin(), cos())
-  const double tn = tan(lat);
-#else
   double tn;
-#if RWRT_RHS_TRIG_SMALL
-  // |lat| >= 2^30, inf or NaN: the ray is masked (|lat| >= pi/2) or its
-  // lookup is NaN, so every output is NaN whatever s, c, tn are -- no
-  // library fallback needed here
-  rwrt_math::rm_sincostan_small(lat, s, c, tn);
-#else
-  sincostan(lat, s, c, tn);         // == sin(), cos(), tan(), one reduction
-#endif
-#endif
+  k_sincostan(lat, s, c, tn);       // np.cos, np.sin, np.tan of lat (bs.py:856-880)
 #endif
 #if RWRT_DIAG_NOINTERP   // timing-only diagnostic build: constant background
 #pragma unroll
@@ -1035,7 +1114,7 @@ __device__ __forceinline__ void ugvg_at(const BG& B, double t, double lon, doubl
                                         double l, double& ug, double& vg) {
   double fu, fv, fqx, fqy;
   B.interp4(lon, lat, t, fu, fv, fqx, fqy);
-  const double c = cos(lat);
+  const double c = k_cos(lat);
   const double m = (fabs(c) <= 0.0175) ? 0.0 : 1.0;
   const double cp = c * m + (1.0 - m) * 1e-6;
   ugvg((fu / cp) * m, (fv / cp) * m, fqx * m, (fqy * cp) * m, k, l, ug, vg);
@@ -1043,16 +1122,16 @@ __device__ __forceinline__ void ugvg_at(const BG& B, double t, double lon, doubl
 
 // cal_dis (wr.py:97-112): haversine between consecutive stored positions
 __device__ __forceinline__ double cal_dis(double lon_c, double lat_c, double lon_p, double lat_p) {
-  const double sd = sin((lat_c - lat_p) / 2.0);
-  const double sl = sin((lon_c - lon_p) / 2.0);
-  const double a = sd * sd + (cos(lat_p) * cos(lat_c)) * (sl * sl);
+  const double sd = k_sin((lat_c - lat_p) / 2.0);
+  const double sl = k_sin((lon_c - lon_p) / 2.0);
+  const double a = sd * sd + (k_cos(lat_p) * k_cos(lat_c)) * (sl * sl);
   return fabs(2.0 * atan2(sqrt(a), sqrt(1.0 - a)));
 }
 // the same with cos(lat_p), cos(lat_c) supplied by the caller
 __device__ __forceinline__ double cal_dis_c(double lon_c, double lat_c, double lon_p, double lat_p,
                                             double cos_c, double cos_p) {
-  const double sd = sin((lat_c - lat_p) / 2.0);
-  const double sl = sin((lon_c - lon_p) / 2.0);
+  const double sd = k_sin((lat_c - lat_p) / 2.0);
+  const double sl = k_sin((lon_c - lon_p) / 2.0);
   const double a = sd * sd + (cos_p * cos_c) * (sl * sl);
   return fabs(2.0 * atan2(sqrt(a), sqrt(1.0 - a)));
 }
@@ -1061,6 +1140,10 @@ __device__ __forceinline__ double cal_dis_c(double lon_c, double lat_c, double l
 // sin() of two arguments through the one-reduction routine (== sin() for
 // |x| < 2^30), with one shared fallback branch to the library for the rest
 __device__ __forceinline__ void sin2(double a, double b, double& sa, double& sb) {
+#if RWRT_MATH_NUMPY
+  sa = k_sin(a);
+  sb = k_sin(b);
+#else
   double c, t;
   rwrt_math::rm_sincostan_small(a, sa, c, t);
   rwrt_math::rm_sincostan_small(b, sb, c, t);
@@ -1069,13 +1152,17 @@ __device__ __forceinline__ void sin2(double a, double b, double& sa, double& sb)
     sa = sin(a);
     sb = sin(b);
   }
+#endif
 }
-// cos() through the one-reduction routine for an argument known to be below
-// pi/2 in magnitude or NaN (no fallback needed: NaN -> NaN)
+// cos() of an argument known to be below pi/2 in magnitude or NaN
 __device__ __forceinline__ double cos_small(double x) {
+#if RWRT_MATH_NUMPY
+  return k_cos(x);
+#else
   double sn, cs, tn;
   rwrt_math::rm_sincostan_small(x, sn, cs, tn);
   return cs;
+#endif
 }
 __device__ __forceinline__ bool cal_dis_reaches(double lon_c, double lat_c, double lon_p,
                                                 double lat_p, double cos_c, double cos_p,
@@ -1125,7 +1212,7 @@ struct KatExp {
   static constexpr int NAUX = 0;
   static constexpr bool kAutonomous = false;
   __device__ void operator()(double t, const double* y, double* dy, double* = nullptr) const {
-    dy[0] = pow(2.718281828459045, 0.1 * t) + y[0] * 0.0;  // np.e ** (0.1 * t)
+    dy[0] = k_pow(2.718281828459045, 0.1 * t) + y[0] * 0.0;  // np.e ** (0.1 * t)
   }
 };
 struct KatLorenz {
@@ -1332,7 +1419,7 @@ __device__ __forceinline__ double initial_step(const P& fun, double t0, const do
     h1 = np_max(1e-6, h0 * 1e-3);
   } else {
     const double dm = (d1 != d1) ? d2 : ((d2 != d2) ? d1 : (d1 >= d2 ? d1 : d2));  // nanmax
-    h1 = rm_pow(0.01 / dm, 0.2);
+    h1 = k_pow(0.01 / dm, 0.2);
   }
   return np_min(100.0 * h0, h1);
 }
@@ -1386,7 +1473,7 @@ struct Lane {
     // SAFETY * error_norm ** (-1/5), shared by the accept (rkf45.py:453-469) and
     // reject (rkf45.py:471-475) factors: one pow per attempt even when the
     // wave's lanes split between the two outcomes
-    const double sp = kSafety * rm_pow(en, kErrExp);
+    const double sp = kSafety * k_pow(en, kErrExp);
 #endif
     // Accept / reject as selects: the lanes of a wave usually disagree, and
     // a branch pair would execute both sides anyway.
@@ -1432,8 +1519,8 @@ __global__ void mercator_kernel(Field F, int64_t n, const double* __restrict__ l
     const double la = lat[i];
     double g[11], o[12];
     interp11(F, py_mod_2pi(lon[i]), la, g);
-    const Merc M = merc_factors(la, cos(la), sin(la));
-    mercator12(g, M, tan(la), o);
+    const Merc M = merc_factors(la, k_cos(la), k_sin(la));
+    mercator12(g, M, k_tan(la), o);
 #pragma unroll
     for (int q = 0; q < 12; ++q) out[q * n + i] = o[q];
   }
@@ -1635,7 +1722,7 @@ __global__ void __launch_bounds__(256, RWRT_WAVES_PER_SIMD) rk45_run_kernel(RunA
       it = a.it_begin;
       prev_lon = L.y[0];   // == rlon[it-1], rlat[it-1] (wr.py:844, 877-885)
       prev_lat = L.y[1];
-      cos_prev = cos(prev_lat);
+      cos_prev = k_cos(prev_lat);
       L.aux[2] = kNaN;     // no evaluation at y yet
     }
     const double tb = a.tbound[it];
@@ -1771,7 +1858,7 @@ frozen_fill_kernel(RunArgs<BG> a) {
     int32_t nanrow = a.nanrow[ray];
     const int32_t it = a.it_begin;
     const double prev_lon = y[0], prev_lat = y[1];
-    const double cos_prev = cos(prev_lat);
+    const double cos_prev = k_cos(prev_lat);
     const double tb = a.tbound[it];
     double ug, vg, cos_c = kNaN;
     bool masked = fabs(y[1]) >= kHalfPi;
@@ -1849,6 +1936,15 @@ __global__ void math_kernel(int kind, int64_t n, const double* __restrict__ x,
     case 22: r = recip2(a); break;
     case 23: { double q1, q2; div2(a, b, b, a, q1, q2); r = q1; } break;
     case 24: { double q1, q2; div2(b, a, a, b, q1, q2); r = q2; } break;
+    case 25: r = np_math::nm_sin(a); break;
+    case 26: r = np_math::nm_cos(a); break;
+    case 27: r = np_math::nm_tan(a); break;
+    case 28: r = np_math::nm_pow(a, b); break;
+    case 29: r = np_math::nm_rcp14(a); break;
+    case 30: { double sn, cs, tn; k_sincostan(a, sn, cs, tn); r = sn; } break;
+    case 31: { double sn, cs, tn; k_sincostan(a, sn, cs, tn); r = cs; } break;
+    case 32: { double sn, cs, tn; k_sincostan(a, sn, cs, tn); r = tn; } break;
+    case 33: r = k_pow(a, b); break;
     default: r = fmod_pos(a, b); break;
   }
   out[i] = r;
@@ -2820,7 +2916,7 @@ rwrt_status rwrt_kat_rk45(int32_t kind, int64_t ncol, const double* d_y0, int32_
 
 rwrt_status rwrt_selftest_math(int32_t kind, int64_t n, const double* d_x, const double* d_y,
                                double* d_out, void* stream) {
-  if (n < 0 || kind < 0 || kind > 24 || (n > 0 && (!d_x || !d_out)))
+  if (n < 0 || kind < 0 || kind > 33 || (n > 0 && (!d_x || !d_out)))
     return fail(RWRT_ERR_ARG, "bad selftest arguments%s");
   if (n == 0) return RWRT_OK;
   hipLaunchKernelGGL(math_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, kind,

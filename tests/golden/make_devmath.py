@@ -1,14 +1,15 @@
-"""Generate tests/golden/devmath_*.npz: the oracle's C2 histories computed with
-the DEVICE's transcendentals (``rwrt_oracle.device_math()``: sin/cos/tan/power
-from oracle/devmath.cpp, the kernel's rwrt_math.h compiled for the host).
+"""Generate tests/golden/ref90_C2_*.npz: the reference's 90-day C2 histories,
+computed by the oracle with NumPy's own transcendentals (the reference's
+arithmetic: the oracle is pinned bit-exact to the reference by
+tests/test_oracle_golden.py).
 
-    make -C oracle && python tests/golden/make_devmath.py
+    python tests/golden/make_devmath.py
 
 The GPU must reproduce these histories bit for bit, every row of 90 days
-(tests/test_gpu_devmath.py): with libm taken out of the comparison, the GPU
-and the NumPy restatement of the reference (pinned bit-exact to the reference
-by tests/test_oracle_golden.py) compute the same numbers.  The inputs are the
-reference's own C2 initial rows (init_C2_<kind>.npz).
+(tests/test_gpu_devmath.py): its sin/cos/tan/pow are NumPy's, restated
+(csrc/np_math.h), and every other operation is the reference's in the
+reference's order.  The inputs are the reference's own C2 initial rows
+(init_C2_<kind>.npz).
 
 Each fixture holds, per output row, the sha256 of the 7 history variables
 (``(7, nray)`` fp64, NaN canonicalised), the last row in full and the
@@ -46,11 +47,11 @@ def main():
         rows = g["rows"].reshape(7, -1)
         ob = O.Background(**S.background(kind))
         t0 = time.time()
-        with np.errstate(all="ignore"), O.device_math():
+        with np.errstate(all="ignore"):
             hist, nacc, nrej, st = O.ray_run(ob, rows[:5].copy(), NT, TSTEP, row0=rows)
             hist4, st4 = O.ray_run_rk4(ob, rows[:5].copy(), NT, TSTEP, row0=rows)
         assert st == 0 and st4 == 0
-        np.savez_compressed(os.path.join(HERE, f"devmath_C2_{kind}.npz"),
+        np.savez_compressed(os.path.join(HERE, f"ref90_C2_{kind}.npz"),
                             nt=NT, row_sha=row_hashes(hist), last=hist[:, -1], nacc=nacc,
                             nrej=nrej, rk4_row_sha=row_hashes(hist4), rk4_last=hist4[:, -1])
         print(kind, f"{time.time() - t0:.0f} s", int(nacc.sum()), "accepted steps")

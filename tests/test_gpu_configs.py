@@ -4,27 +4,26 @@ configs[2..4]) against the oracle.
 * C3 -- the full 2.40 M-slot C3 set integrated 12 days on the GPU; on a
   cost-stratified sample of 16 384 live rays (tests/golden/c3_sample.npz, made
   by tools/c3_sample.py: the 512 rays with the most attempts in day 1 plus
-  random rays from 31 cost quantiles) every row must equal the oracle run on
-  the device's transcendentals BIT FOR BIT (all 7 variables, 144 rows,
-  accepted-step counts), and the distance to the NumPy oracle (the reference's
-  own arithmetic) must stay within the tiers of DESIGN.md §2, judged against
-  the reference's own 1-ulp noise floor measured ON THIS SAMPLE
-  (tests/golden/noise_floor_C3_zonal.json).
+  random rays from 31 cost quantiles) every row must equal the oracle (the
+  reference's own arithmetic, NumPy's transcendentals included) BIT FOR BIT:
+  all 7 variables, 144 rows, accepted-step counts.  (For scale: under a
+  1-ulp RHS perturbation the reference itself moves these rays by up to
+  1.8e-4 rad after a day and 3.6e-2 rad after 12 days,
+  tests/golden/noise_floor_C3_zonal.json.)
 * C4 -- the same sample as ONE ray set split over a world-2 group by measured
   cost (shard.run_sharded: probe launch, snake deal, per-rank integration,
   gather to rank 0), bit-identical to the 1-GPU run.
 * C5 -- 0.25-degree time-varying background, 4 096 live rays from the C5 seed
   grid, 2 days through 9 levels, fp64 and fp32 level storage, bit-identical to
-  the oracle's TimeVaryingBackground on the device's transcendentals.
+  the oracle's TimeVaryingBackground.
 """
-import json
 import os
 import socket
 
 import numpy as np
 import pytest
 
-from conftest import GOLDEN, golden
+from conftest import golden
 
 pytestmark = pytest.mark.gpu
 C3_DAYS = 12
@@ -68,10 +67,10 @@ def c3_run():
     return _C3["gpu"]
 
 
-def test_c3_sample_bitwise_with_device_math():
+def test_c3_sample_bitwise_with_reference_arithmetic():
     import rwrt_oracle as O
     hist, nacc, y0, bg, nt = c3_run()
-    with np.errstate(all="ignore"), O.device_math():
+    with np.errstate(all="ignore"):
         ref, rnacc, _, st = O.ray_run(O.Background(**bg), y0.copy(), nt, 7200.0)
     assert st == 0
     g = np.transpose(hist[:, :, :7], (2, 1, 0))
@@ -79,31 +78,6 @@ def test_c3_sample_bitwise_with_device_math():
     assert np.array_equal(nacc, rnacc)
     # the nacc column of every row is the running accepted-step count
     assert np.array_equal(hist[:, -1, 7].astype(np.int64), rnacc)
-
-
-def test_c3_sample_vs_reference_arithmetic():
-    """Distance to the NumPy oracle (bit-exact with the reference) per horizon,
-    against the reference's own spread under a 1-ulp RHS perturbation."""
-    import rwrt_oracle as O
-    hist, nacc, y0, bg, nt = c3_run()
-    floor = json.load(open(os.path.join(GOLDEN, "noise_floor_C3_zonal.json")))
-    with np.errstate(all="ignore"):
-        ref, rnacc, _, st = O.ray_run(O.Background(**bg), y0.copy(), nt, 7200.0)
-    report = {}
-    for row, key in ((1, "0.0833333d"), (12, "1d"), (48, "4d"), (nt - 1, f"{(nt - 1) / 12:g}d")):
-        a, b = hist[:, row - 1, :2], ref[:2, row].T
-        flips = int(np.sum(np.isnan(a[:, 0]) != np.isnan(b[:, 0])))
-        ok = ~np.isnan(a).any(1) & ~np.isnan(b).any(1)
-        d = np.max(np.abs(a[ok] - b[ok]), axis=1)
-        f = floor[key]
-        report[key] = (float(np.percentile(d, 99)), float(d.max()), flips)
-        if row == 1:   # T2: every ray within the north-star tolerance after one step interval
-            assert d.max() <= 1e-6 and flips == 0, report
-        else:          # T2/T3: within 3x the reference's own spread on this sample
-            assert np.percentile(d, 99) <= max(3 * f["p99"], 1e-12), report
-            assert d.max() <= max(3 * f["max"], 1e-12), report
-            assert flips <= max(3 * f["alive_flips"], len(d) // 1000), report
-    print("C3 sample vs reference arithmetic (p99, max, alive flips):", report)
 
 
 # ---------------------------------------------------------------- C4
@@ -176,7 +150,7 @@ def test_c4_cost_sharded_world2_equals_single_gpu():
 
 # ---------------------------------------------------------------- C5
 @pytest.mark.parametrize("fp32", [False, True])
-def test_c5_025deg_bitwise_with_device_math(fp32):
+def test_c5_025deg_bitwise_with_oracle(fp32):
     import torch
     import rwrt_oracle as O
     import synthetic as S
@@ -202,7 +176,7 @@ def test_c5_025deg_bitwise_with_device_math(fp32):
     del eng, lv
     torch.cuda.empty_cache()
     ob = O.TimeVaryingBackground([O.Background(**b) for b in bl], 0.0, dt, fp32=fp32)
-    with np.errstate(all="ignore"), O.device_math():
+    with np.errstate(all="ignore"):
         ref, nacc, _, st = O.ray_run(ob, y0.copy(), nt, 7200.0)
     assert st == 0
     g = np.transpose(hist[:, :, :7], (2, 1, 0))

@@ -1,5 +1,5 @@
-"""Edge cases of the ray loop on the GPU, bitwise against the oracle on the
-device's own sin/cos/tan/pow (``rwrt_oracle.device_math()``).
+"""Edge cases of the ray loop on the GPU, bitwise against the oracle (the
+reference's arithmetic: the kernels' sin/cos/tan/pow are NumPy's own).
 
 * empty batches (nray = 0) launch nothing and return empty results;
 * ragged batch sizes around the block and fill-tile sizes (1, 127, 129, 300
@@ -48,11 +48,7 @@ def _gpu_rows(eng, y0, nt, chunk):
 
 def _oracle(bg, y0, nt):
     import rwrt_oracle as O
-    try:
-        O._devmath_lib()
-    except (RuntimeError, OSError) as e:
-        pytest.skip(f"oracle/_devmath not built: {e}")
-    with np.errstate(all="ignore"), O.device_math():
+    with np.errstate(all="ignore"):
         hist, nacc, nrej, status = O.ray_run(O.Background(**bg), y0.copy(), nt, 7200.0)
     return hist, nacc, nrej, status
 
@@ -164,10 +160,6 @@ def test_rk4_chunked_runs_equal_one_launch():
     assert _same(h1[:, 1:], h2[:, 1:])
     assert torch.equal(r1.nacc, r2.nacc) and torch.equal(r1.nrej, r2.nrej)
     assert torch.equal(r1.nanrow, r2.nanrow)
-    try:
-        O._devmath_lib()
-    except (RuntimeError, OSError) as e:
-        pytest.skip(f"oracle/_devmath not built: {e}")
-    with np.errstate(all="ignore"), O.device_math():
+    with np.errstate(all="ignore"):
         href, _ = O.ray_run_rk4(O.Background(**bg), rows7[:5].copy(), nt, 7200.0, row0=rows7)
     assert _same(np.transpose(h2[:, 1:, :7], (2, 1, 0)), href[:, 1:])
