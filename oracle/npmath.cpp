@@ -37,20 +37,12 @@ static inline double add_rd(double a, double b) {
 #define NM_MUL_RZ(a, b) mul_rz((a), (b))
 #define NM_ADD_RZ(a, b) add_rz((a), (b))
 #define NM_ADD_RD(a, b) add_rd((a), (b))
-#define NM_RCP14_TAB g_rcp14.v
 #define NM_FALLBACK_SIN(x) std::sin(x)
 #define NM_FALLBACK_COS(x) std::cos(x)
 #define NM_FALLBACK_TAN(x) std::tan(x)
 #define NM_FALLBACK_POW(x, y) std::pow((x), (y))
-namespace np_math {
-struct NmRcp14;
-extern const NmRcp14 g_rcp14;
-}
 #include "np_math.h"
 
-namespace np_math {
-constexpr NmRcp14 g_rcp14 = nm_rcp14_table();
-}
 using namespace np_math;
 
 extern "C" {
@@ -67,6 +59,12 @@ void nm_tan_arr(const double* x, double* out, int64_t n) {
 // x ** y element-wise (y broadcast when ystride == 0)
 void nm_pow_arr(const double* x, const double* y, int64_t ystride, double* out, int64_t n) {
   for (int64_t i = 0; i < n; ++i) out[i] = nm_pow(x[i], y[i * ystride]);
+}
+void nm_sincos_arr(const double* x, double* s, double* c, int64_t n) {
+  for (int64_t i = 0; i < n; ++i) nm_sincos(x[i], s[i], c[i]);
+}
+void nm_sincostan_arr(const double* x, double* s, double* c, double* t, int64_t n) {
+  for (int64_t i = 0; i < n; ++i) nm_sincostan(x[i], s[i], c[i], t[i]);
 }
 void nm_rcp14_arr(const double* x, double* out, int64_t n) {
   for (int64_t i = 0; i < n; ++i) out[i] = nm_rcp14(x[i]);

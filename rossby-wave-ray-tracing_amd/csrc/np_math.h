@@ -29,8 +29,6 @@
 //   NM_FMA_RZ(a,b,c) fused multiply-add rounded toward zero
 //   NM_ADD_RZ(a,b)   addition rounded toward zero
 //   NM_MUL_RZ(a,b)   multiplication rounded toward zero
-//   NM_RCP14_TAB     the expanded VRCP14PD table (nm_rcp14_table(): 65536 x
-//                    uint16 result fraction bits), declared after this header
 //   NM_ADD_RD(a,b)   addition rounded toward -infinity
 //   NM_FALLBACK_SIN/COS/TAN/POW  library routines outside the domain above
 // Compile with -ffp-contract=off: every fused operation here is explicit.
@@ -40,8 +38,6 @@
 
 namespace np_math {
 
-struct NmRcp14;
-
 NM_FN double nm_d(unsigned long long u) { return __builtin_bit_cast(double, u); }
 NM_FN unsigned long long nm_u(double x) { return __builtin_bit_cast(unsigned long long, x); }
 NM_FN double nm_fma(double a, double b, double c) { return __builtin_fma(a, b, c); }
@@ -50,38 +46,48 @@ NM_FN double nm_sign(double x) { return nm_d(nm_u(x) & 0x8000000000000000ull); }
 NM_FN double nm_copysign(double m, double s) {
   return nm_d((nm_u(m) & 0x7FFFFFFFFFFFFFFFull) | (nm_u(s) & 0x8000000000000000ull));
 }
-NM_FN double tabd(const unsigned long long* t, int i) { return nm_d(t[i]); }
+// Table reads go through NM_LD(table, i) (default: the array element); an
+// includer can serve them from a faster copy (e.g. LDS).
+//
+// The common path of each function is straight-line code (the arms of the
+// reference's data-dependent branches computed both and selected, table
+// indices clamped into range), with the rare arguments fixed up at the end:
+// on the GPU a wave then never splits on the argument ranges of its lanes
+// and the table reads can be issued early.  The selected values are the
+// reference's; what differs is only which dead values get computed.
+#ifndef NM_LD
+#define NM_LD(t, i) (t)[i]
+#endif
+#define tabd(t, i) nm_d(NM_LD(t, i))
+// NM_ISSUE_FENCE(): the table reads above it are issued before the work below
+// (e.g. a scheduling barrier); nothing on the host
+#ifndef NM_ISSUE_FENCE
+#define NM_ISSUE_FENCE()
+#endif
 
 // ---------------------------------------------------------------------------
 // VRCP14PD: the result depends on the sign, the exponent and the top 16
-// fraction bits of the input (an exact power of two has its exact
-// reciprocal); the 16-bit result fraction comes from the table.  Normal
-// inputs whose reciprocal is normal.
+// fraction bits i of the input; its 16 fraction bits are the fixed-point
+// interpolation (A[k] - N[k] o) >> 10, k = i >> 10, o = i & 1023 (knots
+// recovered from the instruction itself for every i, tools/gen_np_math.py).
+// An exact power of two has its exact reciprocal.  Normal inputs whose
+// reciprocal is normal.
 // ---------------------------------------------------------------------------
-// The expanded table: entry i = the 16 result fraction bits for inputs with
-// top fraction bits i; built at compile time from the 2-bit deltas of
-// np_math_tables.h (the includer stores one: a __device__ const on the GPU).
-struct NmRcp14 {
-  unsigned short v[65536];
-};
-constexpr NmRcp14 nm_rcp14_table() {
-  NmRcp14 t{};
-  unsigned f = kRCP14_F0;
-  t.v[0] = (unsigned short)f;
-  for (int i = 1; i < 65536; ++i) {
-    const int k = i - 1;
-    f -= (kRCP14_DELTA[k >> 4] >> (2 * (k & 15))) & 3u;
-    t.v[i] = (unsigned short)f;
-  }
-  return t;
-}
-NM_FN double nm_rcp14(double x) {
+// (rcp14_knot: the knot index of x; nm_rcp14_k: the reciprocal given its knots)
+NM_FN unsigned rcp14_knot(double x) { return 2u * ((unsigned)(nm_u(x) >> 46) & 63u); }
+NM_FN double nm_rcp14_k(double x, unsigned A, unsigned N) {
   const unsigned long long u = nm_u(x);
   const unsigned long long e = (u >> 52) & 0x7FF;
-  const unsigned i = (unsigned)(u >> 36) & 0xFFFF;
   const unsigned long long s = u & 0x8000000000000000ull;
-  if ((u & 0x000FFFFFFFFFFFFFull) == 0) return nm_d(s | ((2046ull - e) << 52));   // 2^-(e-1023)
-  return nm_d(s | ((2045ull - e) << 52) | ((unsigned long long)NM_RCP14_TAB[i] << 36));
+  const unsigned o = (unsigned)(u >> 36) & 1023u;
+  const unsigned f = (A - N * o) >> 10;
+  const double p2 = nm_d(s | ((2046ull - e) << 52));          // 2^-(e-1023)
+  const double r = nm_d(s | ((2045ull - e) << 52) | ((unsigned long long)f << 36));
+  return (u & 0x000FFFFFFFFFFFFFull) == 0 ? p2 : r;
+}
+NM_FN double nm_rcp14(double x) {
+  const unsigned k = rcp14_knot(x);
+  return nm_rcp14_k(x, NM_LD(kRCP14_KNOT, k), NM_LD(kRCP14_KNOT, k + 1));
 }
 
 // ---------------------------------------------------------------------------
@@ -97,13 +103,27 @@ NM_FN double g_taylor_sin(double a, double da) {
   const double t1 = nm_fma(p, a, -(da * nm_d(kG_CS2)));     // vfmsub: P a - 0.5 da
   return a + nm_fma(xx, t1, da);
 }
-// do_sin(x, dx): |x| >= 0.126 here unless the Taylor branch is taken
-NM_FN double g_do_sin(double x, double dx) {
-  if (nm_abs(x) < nm_d(kG_T126)) return g_taylor_sin(x, dx);
-  if (!(0.0 < x)) dx = -dx;                                   // x <= 0 (or NaN)
+// sincostab index of the table point nearest |x| (x + BIG rounds |x| to
+// 1/128); clamped for arguments off the table (their value is not selected)
+NM_FN unsigned g_index(double x) {
+  const unsigned k = (unsigned)nm_u(nm_d(kG_BIG) + nm_abs(x)) << 2;
+  return k < 436u ? k : 436u;
+}
+// sin and cos of the table point k as double-doubles
+struct GTab {
+  double sn, ssn, cs, ccs;
+};
+NM_FN GTab g_tab(unsigned k) {
+  return GTab{tabd(kG_SINCOSTAB, k), tabd(kG_SINCOSTAB, k + 1), tabd(kG_SINCOSTAB, k + 2),
+              tabd(kG_SINCOSTAB, k + 3)};
+}
+// do_sin(x, dx) with the table entry of x fetched by the caller (below 0.126
+// the Taylor branch's value is returned)
+NM_FN double g_do_sin_t(double x, double dx, const GTab& T) {
+  const double ts = g_taylor_sin(x, dx);                      // |x| < 0.126
+  dx = (0.0 < x) ? dx : -dx;                                  // x <= 0 (or NaN): -dx
   const double ax = nm_abs(x);
   const double u = nm_d(kG_BIG) + ax;
-  const int k = (int)((unsigned)nm_u(u) << 2);
   const double xr = ax - (u - nm_d(kG_BIG));
   const double xx = xr * xr;
   const double t = nm_fma(nm_d(kG_SN5), xx, nm_d(kG_SN3));
@@ -111,17 +131,14 @@ NM_FN double g_do_sin(double x, double dx) {
   double c0 = nm_fma(nm_d(kG_CS6), xx, nm_d(kG_CS4));
   c0 = nm_fma(c0, xx, nm_d(kG_CS2));
   const double c = nm_fma(xr, dx, xx * c0);
-  const double sn = tabd(kG_SINCOSTAB, k), ssn = tabd(kG_SINCOSTAB, k + 1);
-  const double cs = tabd(kG_SINCOSTAB, k + 2), ccs = tabd(kG_SINCOSTAB, k + 3);
-  const double cor = nm_fma(s, cs, nm_fma(-c, sn, nm_fma(ccs, s, ssn)));
-  return nm_copysign(sn + cor, x);
+  const double cor = nm_fma(s, T.cs, nm_fma(-c, T.sn, nm_fma(T.ccs, s, T.ssn)));
+  return nm_abs(x) < nm_d(kG_T126) ? ts : nm_copysign(T.sn + cor, x);
 }
-// do_cos(x, dx)
-NM_FN double g_do_cos(double x, double dx) {
-  if (x < 0.0) dx = -dx;
+// do_cos(x, dx), the same
+NM_FN double g_do_cos_t(double x, double dx, const GTab& T) {
+  dx = (x < 0.0) ? -dx : dx;
   const double ax = nm_abs(x);
   const double u = nm_d(kG_BIG) + ax;
-  const int k = (int)((unsigned)nm_u(u) << 2);
   const double xr = (ax - (u - nm_d(kG_BIG))) + dx;
   const double xx = xr * xr;
   const double t = nm_fma(nm_d(kG_SN5), xx, nm_d(kG_SN3));
@@ -129,11 +146,11 @@ NM_FN double g_do_cos(double x, double dx) {
   double c0 = nm_fma(nm_d(kG_CS6), xx, nm_d(kG_CS4));
   c0 = nm_fma(c0, xx, nm_d(kG_CS2));
   const double c = xx * c0;
-  const double sn = tabd(kG_SINCOSTAB, k), ssn = tabd(kG_SINCOSTAB, k + 1);
-  const double cs = tabd(kG_SINCOSTAB, k + 2), ccs = tabd(kG_SINCOSTAB, k + 3);
-  const double cor = nm_fma(-s, sn, nm_fma(-c, cs, nm_fma(-s, ssn, ccs)));
-  return cs + cor;
+  const double cor = nm_fma(-s, T.sn, nm_fma(-c, T.cs, nm_fma(-s, T.ssn, T.ccs)));
+  return T.cs + cor;
 }
+NM_FN double g_do_sin(double x, double dx) { return g_do_sin_t(x, dx, g_tab(g_index(x))); }
+NM_FN double g_do_cos(double x, double dx) { return g_do_cos_t(x, dx, g_tab(g_index(x))); }
 // reduce_sincos: x = n pi/2 + (a + da), n mod 4
 NM_FN int g_reduce(double x, double& a, double& da) {
   const double t = nm_fma(x, nm_d(kG_HPINV), nm_d(kG_TOINT));
@@ -187,18 +204,66 @@ NM_FN double nm_cos(double x) {
   return NM_FALLBACK_COS(x);
 }
 
+// sin and cos of one argument, bit for bit nm_sin(x) and nm_cos(x), with the
+// work shared: below |x| = 2.426265 (every latitude) each of the two is one
+// of glibc's do_sin / do_cos evaluations, and the pair is always one of each
+// -- (do_sin(x, 0), do_cos(x, 0)) below 0.855469, (do_cos(pi/2 - |x|, pi/2
+// tail), do_sin of the same point as a double-double) above -- so a lane
+// evaluates exactly one do_sin and one do_cos whichever range it is in.
+// (without the arguments |x| >= 2.426265, inf and NaN: nm_sincos below)
+// split so that a caller can place work between the table reads and their
+// use: nm_sincos_tab issues the two lookups, nm_sincos_fin evaluates
+struct SinCosPre {
+  GTab Ts, Tc;
+};
+NM_FN SinCosPre nm_sincos_tab(double x) {
+  const bool far = g_hi(x) >= 0x3FEB6000u;
+  const double t = nm_d(kG_HP0) - nm_abs(x);
+  const double a = t + nm_d(kG_HP1);
+  return SinCosPre{g_tab(g_index(far ? a : x)), g_tab(g_index(far ? t : x))};
+}
+NM_FN void nm_sincos_fin(double x, const SinCosPre& P, double& sn, double& cs) {
+  const unsigned k = g_hi(x);
+  const bool far = k >= 0x3FEB6000u;
+  const double t = nm_d(kG_HP0) - nm_abs(x);
+  const double a = t + nm_d(kG_HP1);
+  const double da = (t - a) + nm_d(kG_HP1);
+  const double S = g_do_sin_t(far ? a : x, far ? da : 0.0, P.Ts);
+  const double C = g_do_cos_t(far ? t : x, far ? nm_d(kG_HP1) : 0.0, P.Tc);
+  sn = far ? nm_copysign(C, x) : S;
+  cs = far ? S : C;
+  sn = (k < 0x3E500000u) ? x : sn;
+  cs = (k < 0x3E400000u) ? 1.0 : cs;
+}
+NM_FN void nm_sincos_main(double x, double& sn, double& cs) {
+  const SinCosPre P = nm_sincos_tab(x);
+  NM_ISSUE_FENCE();
+  nm_sincos_fin(x, P, sn, cs);
+}
+NM_FN bool nm_sincos_rare(double x) { return !(g_hi(x) < 0x400368FDu); }
+NM_FN void nm_sincos(double x, double& sn, double& cs) {
+  nm_sincos_main(x, sn, cs);
+  if (nm_sincos_rare(x)) {                                    // |x| >= 2.426265, inf, NaN (rare)
+    sn = nm_sin(x);
+    cs = nm_cos(x);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // SVML __svml_tan8_ha (main path, |x| <= 65536): x = n pi/16 + r,
 // tan x = (T + tan r) / (1 - T tan r), T = tan(n pi/16) in head + tail
 // ---------------------------------------------------------------------------
-NM_FN double nm_tan(double x) {
-  if (!(nm_abs(x) <= nm_d(kT_BIGARG))) {
-    if (x != x || nm_abs(x) == __builtin_inf()) return x - x;   // NaN
-    return NM_FALLBACK_TAN(x);
-  }
+// (without |x| > 65536, inf and NaN: nm_tan below).  t_index: the table
+// point j of x; nm_tan_t: tan x given T = tan(j pi/16) as head + tail.
+NM_FN int t_index(double x) { return (int)(nm_u(nm_fma(nm_d(kT_INVPI16), x, nm_d(kT_SHIFT))) & 15); }
+// in two stages around the reciprocal's knot read: nm_tan_pre up to D = 1 -
+// T tan r, nm_tan_fin from rcp14(D) on
+struct TanPre {
+  double N, Nl, D, dl;
+};
+NM_FN TanPre nm_tan_pre(double x, double T, double Tl) {
   const double y = nm_fma(nm_d(kT_INVPI16), x, nm_d(kT_SHIFT));
   const double n = y - nm_d(kT_SHIFT);
-  const int j = (int)(nm_u(y) & 15);
   const double r1 = nm_fma(-n, nm_d(kT_PI16A), x);
   const double r2 = nm_fma(-n, nm_d(kT_PI16B), r1);
   const double r = nm_fma(-n, nm_d(kT_PI16C), r2);
@@ -214,7 +279,6 @@ NM_FN double nm_tan(double x) {
   const double z9 = nm_fma(-r2q, pr, -rl);                    // vfnmsub: -(r^2 p r) - rl
   const double th = r - z9;                                   // tan r, head
   const double tl = (r - th) - z9;                            // and tail
-  const double T = tabd(kT_TAN_HI, j), Tl = tabd(kT_TAN_LO, j);
   const double N = th + T;
   const double nl = (th - (N - T)) + Tl;
   const double D = nm_fma(-th, T, nm_d(kT_ONE));
@@ -222,14 +286,54 @@ NM_FN double nm_tan(double x) {
   double dl = nm_fma(th, T, D - nm_d(kT_ONE));
   dl = nm_fma(tl, T, dl);
   dl = nm_fma(th, Tl, dl);
-  double rc = nm_rcp14(D);
-  double e = nm_fma(-D, rc, nm_d(kT_ONE));
-  e = nm_fma(dl, rc, e);
+  return TanPre{N, Nl, D, dl};
+}
+NM_FN double nm_tan_fin(const TanPre& t, unsigned A, unsigned Nk) {
+  double rc = nm_rcp14_k(t.D, A, Nk);
+  double e = nm_fma(-t.D, rc, nm_d(kT_ONE));
+  e = nm_fma(t.dl, rc, e);
   rc = nm_fma(e, rc, rc);
-  const double q = rc * N;
-  double res = nm_fma(q, D, -N);
-  res = nm_fma(-q, dl, res);
-  return nm_fma(-rc, res - Nl, q);
+  const double q = rc * t.N;
+  double res = nm_fma(q, t.D, -t.N);
+  res = nm_fma(-q, t.dl, res);
+  return nm_fma(-rc, res - t.Nl, q);
+}
+NM_FN double nm_tan_t(double x, double T, double Tl) {
+  const TanPre t = nm_tan_pre(x, T, Tl);
+  const unsigned k = rcp14_knot(t.D);
+  return nm_tan_fin(t, NM_LD(kRCP14_KNOT, k), NM_LD(kRCP14_KNOT, k + 1));
+}
+NM_FN double nm_tan_main(double x) {
+  const int j = t_index(x);
+  return nm_tan_t(x, tabd(kT_TAN_HI, j), tabd(kT_TAN_LO, j));
+}
+NM_FN double nm_tan(double x) {
+  const double v = nm_tan_main(x);
+  if (!(nm_abs(x) <= nm_d(kT_BIGARG)))                        // |x| > 65536, inf, NaN (rare)
+    return (x != x || nm_abs(x) == __builtin_inf()) ? x - x : NM_FALLBACK_TAN(x);
+  return v;
+}
+
+// sin, cos and tan of one argument (the RHS's latitude): one straight-line
+// block for the three, one rare-argument branch
+//   reads: tan's table point, sin/cos's two | tan up to 1 - T tan r, the
+//   reciprocal's knots | sin and cos | tan
+NM_FN void nm_sincostan(double x, double& sn, double& cs, double& tn) {
+  const int j = t_index(x);
+  const double T = tabd(kT_TAN_HI, j), Tl = tabd(kT_TAN_LO, j);
+  const SinCosPre P = nm_sincos_tab(x);
+  NM_ISSUE_FENCE();
+  const TanPre tp = nm_tan_pre(x, T, Tl);
+  const unsigned k = rcp14_knot(tp.D);
+  const unsigned A = NM_LD(kRCP14_KNOT, k), Nk = NM_LD(kRCP14_KNOT, k + 1);
+  NM_ISSUE_FENCE();
+  nm_sincos_fin(x, P, sn, cs);
+  tn = nm_tan_fin(tp, A, Nk);
+  if (nm_sincos_rare(x)) {                                    // |x| >= 2.426265, inf, NaN (rare)
+    sn = nm_sin(x);
+    cs = nm_cos(x);
+    tn = nm_tan(x);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -238,42 +342,47 @@ NM_FN double nm_tan(double x) {
 // rounded to 1/32), T = y log2 x by round-toward-zero double-double steps,
 // 2^T from a 16-entry table and a degree-7 polynomial
 // ---------------------------------------------------------------------------
+// pow's special values: x NaN, 0, inf or < 0, y NaN or inf (C99 / IEEE pow,
+// what SVML's rare path returns)
+NM_FN double nm_pow_special(double x, double y) {
+  const double inf = __builtin_inf();
+  // C99 / IEEE pow special values (what SVML's rare path returns)
+  if (y == 0.0) return 1.0;
+  if (x == 1.0) return 1.0;
+  if (x != x || y != y) return x + y;
+  const double ax = nm_abs(x);
+  const bool yint = __builtin_trunc(y) == y && nm_abs(y) != inf;
+  const bool yodd = yint && nm_abs(y) < 9007199254740992.0 && __builtin_fmod(y, 2.0) != 0.0;
+  if (nm_abs(y) == inf) {
+    if (ax == 1.0) return 1.0;
+    return ((ax < 1.0) == (y < 0.0)) ? inf : 0.0;
+  }
+  if (x == 0.0) {
+    const double v = (y < 0.0) ? inf : 0.0;
+    return yodd ? nm_copysign(v, x) : v;
+  }
+  if (ax == inf) {
+    const double v = (y < 0.0) ? 0.0 : inf;
+    return (x < 0.0 && yodd) ? -v : v;
+  }
+  // finite x < 0
+  if (!yint) return __builtin_nan("");
+  const double m = NM_FALLBACK_POW(ax, y);
+  return yodd ? -m : m;
+}
+
 NM_FN double nm_pow(double x, double y) {
   const double inf = __builtin_inf();
   const bool xs = !(x > 0.0) || x == inf || x != x;           // vfpclass 0xdf: NaN, 0, inf, < 0
   const bool ys = y != y || nm_abs(y) == inf;                  // vfpclass 0x99
-  if (xs || ys) {
-    // C99 / IEEE pow special values (what SVML's rare path returns)
-    if (y == 0.0) return 1.0;
-    if (x == 1.0) return 1.0;
-    if (x != x || y != y) return x + y;
-    const double ax = nm_abs(x);
-    const bool yint = __builtin_trunc(y) == y && nm_abs(y) != inf;
-    const bool yodd = yint && nm_abs(y) < 9007199254740992.0 && __builtin_fmod(y, 2.0) != 0.0;
-    if (nm_abs(y) == inf) {
-      if (ax == 1.0) return 1.0;
-      return ((ax < 1.0) == (y < 0.0)) ? inf : 0.0;
-    }
-    if (x == 0.0) {
-      const double v = (y < 0.0) ? inf : 0.0;
-      return yodd ? nm_copysign(v, x) : v;
-    }
-    if (ax == inf) {
-      const double v = (y < 0.0) ? 0.0 : inf;
-      return (x < 0.0 && yodd) ? -v : v;
-    }
-    // finite x < 0
-    if (!yint) return __builtin_nan("");
-    const double m = NM_FALLBACK_POW(ax, y);
-    return yodd ? -m : m;
-  }
   // vgetmant (interval [0.5, 1)) and vgetexp of x > 0, normal or subnormal
   unsigned long long ux = nm_u(x);
   int ex = (int)((ux >> 52) & 0x7FF) - 1023;
-  if ((ux >> 52) == 0) {                                       // subnormal: normalise
-    const int lz = __builtin_clzll(ux) - 11;
-    ux <<= lz;
-    ex = -1022 - lz;
+  {                                                            // subnormal: normalise
+    const int lz = __builtin_clzll(ux | 1) - 11;
+    const bool sub = (ux >> 52) == 0;
+    ux = sub ? ux << lz : ux;
+    ex = sub ? -1022 - lz : ex;
   }
   const double M = nm_d((ux & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull);   // [1, 2)
   const double m = M * 0.5;                                                          // [0.5, 1)
@@ -315,11 +424,12 @@ NM_FN double nm_pow(double x, double y) {
   const double Pl = NM_FMA_RZ(y, Lt, pe);
   const double T = NM_ADD_RZ(P, Pl);                          // y log2 x
   const double Tl = Pl - (T - P);
-  if (!(nm_abs(T) <= nm_d(kP_TOVF))) return NM_FALLBACK_POW(x, y);   // over/underflow (rare path)
+  const bool ovf = !(nm_abs(T) <= nm_d(kP_TOVF));            // over/underflow (rare path)
   // 2^T: T = (k16 + fr) / 16 with fr in [0, 1) (vaddpd {rd-sae} on a shifter
   // and vreducepd 0x41: both the floor at 1/16)
-  const double fl = __builtin_floor(T * 16.0);
-  const double frac = NM_ADD_RD(T, -(fl * 0.0625));   // vreducepd subtracts under its own RD
+  const double Tm = ovf ? 0.0 : T;                            // (a finite stand-in there)
+  const double fl = __builtin_floor(Tm * 16.0);
+  const double frac = NM_ADD_RD(Tm, -(fl * 0.0625));   // vreducepd subtracts under its own RD
   const long long k16 = (long long)fl;
   const int jj = (int)(k16 & 15);
   const long long kk = k16 >> 4;
@@ -334,7 +444,10 @@ NM_FN double nm_pow(double x, double y) {
   p1 = nm_fma(fz, p1, El);
   p1 = nm_fma(Eh, p1, Eh);
   const double scale = nm_d((unsigned long long)(kk + 1023) << 52);
-  return p1 * scale;
+  const double v = p1 * scale;
+  if (xs || ys) return nm_pow_special(x, y);
+  if (ovf) return NM_FALLBACK_POW(x, y);
+  return v;
 }
 
 }  // namespace np_math

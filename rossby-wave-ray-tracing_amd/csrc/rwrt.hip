@@ -466,6 +466,13 @@ __device__ __forceinline__ char* lds_slice_base(char* wave_base) {
 #endif
 }
 
+// Before end() reads a slice: wait for the refill's LDS-DMA.  Explicit,
+// because the compiler's own wait is not reliable once a kernel holds more
+// than one LDS variable (the NumPy-math tables): its LDS reads then carry
+// alias scopes, and a scoped read is only checked against LDS-DMA stores
+// that carry scopes too -- which these (through lds_slice_base) do not.
+__device__ __forceinline__ void lds_dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
 struct CachedStaticBG {
   static constexpr bool kTimeVarying = false;
   Field F;
@@ -496,6 +503,7 @@ struct CachedStaticBG {
     return Pending{k.wa, k.wb, k.wc, k.wd};
   }
   __device__ __forceinline__ void end(const Pending& p, double g[11]) const {
+    lds_dma_wait();
     Corners k;
     k.wa = p.wa;
     k.wb = p.wb;
@@ -688,6 +696,7 @@ struct CachedVaryingBG32 {
     return p;
   }
   __device__ __forceinline__ void end(const Pending& p, double g[11]) const {
+    lds_dma_wait();
     float4 v[2][4][3];
 #pragma unroll
     for (int lev = 0; lev < 2; ++lev)
@@ -770,6 +779,7 @@ struct CachedVaryingBG64 {
     return p;
   }
   __device__ __forceinline__ void end(const Pending& p, double g[11]) const {
+    lds_dma_wait();
     double gb[11];
     V.blend_level<11>(p.B, p.o, p.w, 0, gb);
     double2 v[4][6];
@@ -888,35 +898,102 @@ __device__ __forceinline__ void sincostan(double x, double& sn, double& cs, doub
 // np.sin/np.cos/np.tan/np.power on the reference's AVX-512 hosts
 // (tests/test_np_math.py on the host, tests/test_gpu_np_math.py here).
 // SVML pow's round-toward-zero / -infinity steps set the f64 round mode for
-// one instruction each (ocml's rounded operations: s_setreg of MODE.FP_ROUND).
+// one instruction each (MODE.FP_ROUND[3:2]: 3 toward zero, 2 toward -inf),
+// inline: the device library's rounded operations are out-of-line calls,
+// and a call waits for every outstanding memory operation at its entry.
+// The s_nops cover the VALU -> s_setreg(MODE) hazard both ways.
 // ---------------------------------------------------------------------------
-extern "C" __device__ double __ocml_fma_rtz_f64(double, double, double);
-extern "C" __device__ double __ocml_mul_rtz_f64(double, double);
-extern "C" __device__ double __ocml_add_rtz_f64(double, double);
-extern "C" __device__ double __ocml_add_rtn_f64(double, double);
+#define RWRT_F64_RM_ASM(op, mode)                                                  \
+  "s_nop 1\n\ts_setreg_imm32_b32 hwreg(HW_REG_MODE, 2, 2), " #mode "\n\t" op       \
+  "\n\ts_nop 1\n\ts_setreg_imm32_b32 hwreg(HW_REG_MODE, 2, 2), 0\n\ts_nop 1"
+namespace rwrt {
+__device__ __forceinline__ double fma_rz(double a, double b, double c) {
+  double r;
+  asm(RWRT_F64_RM_ASM("v_fma_f64 %0, %1, %2, %3", 3) : "=&v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ double mul_rz(double a, double b) {
+  double r;
+  asm(RWRT_F64_RM_ASM("v_mul_f64 %0, %1, %2", 3) : "=&v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ double add_rz(double a, double b) {
+  double r;
+  asm(RWRT_F64_RM_ASM("v_add_f64 %0, %1, %2", 3) : "=&v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ double add_rd(double a, double b) {
+  double r;
+  asm(RWRT_F64_RM_ASM("v_add_f64 %0, %1, %2", 2) : "=&v"(r) : "v"(a), "v"(b));
+  return r;
+}
+}  // namespace rwrt
 #define NM_FN __device__ __forceinline__
 #define NM_CONST constexpr
 #define NM_TABLE constexpr
-#define NM_FMA_RZ(a, b, c) __ocml_fma_rtz_f64((a), (b), (c))
-#define NM_MUL_RZ(a, b) __ocml_mul_rtz_f64((a), (b))
-#define NM_ADD_RZ(a, b) __ocml_add_rtz_f64((a), (b))
-#define NM_ADD_RD(a, b) __ocml_add_rtn_f64((a), (b))
-#define NM_RCP14_TAB ::np_math::g_nm_rcp14.v
+#define NM_FMA_RZ(a, b, c) ::rwrt::fma_rz((a), (b), (c))
+#define NM_MUL_RZ(a, b) ::rwrt::mul_rz((a), (b))
+#define NM_ADD_RZ(a, b) ::rwrt::add_rz((a), (b))
+#define NM_ADD_RD(a, b) ::rwrt::add_rd((a), (b))
+#define NM_ISSUE_FENCE() __builtin_amdgcn_sched_barrier(0)
 #define NM_FALLBACK_SIN(x) ::sin(x)
 #define NM_FALLBACK_COS(x) ::cos(x)
 #define NM_FALLBACK_TAN(x) ::tan(x)
 #define NM_FALLBACK_POW(x, y) ::pow((x), (y))
-namespace np_math {
-struct NmRcp14;
-extern __device__ const NmRcp14 g_nm_rcp14;
-}
+// The tables live in LDS inside the kernels (staged at kernel entry by
+// nm_stage): per-lane table reads from global memory would share vmcnt with
+// the cell cache's LDS-DMA refills, so every read would also wait for the
+// refill the RHS issued before its trigonometry.
+#ifndef RWRT_NM_LDS
+#define RWRT_NM_LDS 1
+#endif
+#if RWRT_DIAG_NM_TAB0    // timing-only diagnostic build: every table read at a lane-uniform index
+#define NM_LD(t, i) (t)[(i) & 0]
+#elif RWRT_NM_LDS
+__shared__ unsigned long long nm_lds_kG_SINCOSTAB[440];
+__shared__ unsigned long long nm_lds_kT_TAN_HI[16];
+__shared__ unsigned long long nm_lds_kT_TAN_LO[16];
+__shared__ unsigned long long nm_lds_kP_LOG_HI[32];
+__shared__ unsigned long long nm_lds_kP_LOG_LO[32];
+__shared__ unsigned long long nm_lds_kP_EXP_HI[16];
+__shared__ unsigned long long nm_lds_kP_EXP_LO[16];
+__shared__ unsigned nm_lds_kRCP14_KNOT[128];
+#define NM_LD(t, i) nm_lds_##t[i]
+#endif
 #include "np_math.h"
-namespace np_math {
-// VRCP14PD's 64 K-entry result table (128 KB), expanded at compile time
-__device__ const NmRcp14 g_nm_rcp14 = nm_rcp14_table();
-}
 
 namespace rwrt {
+// Copies the tables a kernel's math reads into its LDS (every thread of the
+// block must call it, before any other use): NM_SINCOS = glibc's sin/cos
+// table, NM_TAN = SVML tan's tables, NM_POW = SVML pow's (both with the
+// VRCP14 knots).  A no-op when the tables are read from global memory.
+enum { NM_SINCOS = 1, NM_TAN = 2, NM_POW = 4, NM_ALL = 7 };
+template <int MASK>
+__device__ __forceinline__ void nm_stage() {
+#if RWRT_NM_LDS && !RWRT_DIAG_NM_TAB0
+  const int t = threadIdx.x, nt = blockDim.x;
+  if (MASK & NM_SINCOS)
+    for (int i = t; i < 440; i += nt) nm_lds_kG_SINCOSTAB[i] = np_math::kG_SINCOSTAB[i];
+  if (MASK & NM_TAN)
+    for (int i = t; i < 16; i += nt) {
+      nm_lds_kT_TAN_HI[i] = np_math::kT_TAN_HI[i];
+      nm_lds_kT_TAN_LO[i] = np_math::kT_TAN_LO[i];
+    }
+  if (MASK & NM_POW)
+    for (int i = t; i < 32; i += nt) {
+      nm_lds_kP_LOG_HI[i] = np_math::kP_LOG_HI[i];
+      nm_lds_kP_LOG_LO[i] = np_math::kP_LOG_LO[i];
+      if (i < 16) {
+        nm_lds_kP_EXP_HI[i] = np_math::kP_EXP_HI[i];
+        nm_lds_kP_EXP_LO[i] = np_math::kP_EXP_LO[i];
+      }
+    }
+  if (MASK & (NM_TAN | NM_POW))
+    for (int i = t; i < 128; i += nt) nm_lds_kRCP14_KNOT[i] = np_math::kRCP14_KNOT[i];
+  __syncthreads();
+#endif
+}
+
 // The kernels' transcendentals: the reference NumPy's (default) or, in the
 // RWRT_MATH_NUMPY=0 diagnostic build, the device library's algorithms
 // (rwrt_math.h; last-bit different from the reference).
@@ -950,8 +1027,11 @@ __device__ __forceinline__ double k_tan(double x) {
   return t;
 #endif
 }
+#ifndef RWRT_POW_NUMPY
+#define RWRT_POW_NUMPY RWRT_MATH_NUMPY
+#endif
 __device__ __forceinline__ double k_pow(double x, double y) {
-#if RWRT_MATH_NUMPY
+#if RWRT_POW_NUMPY
   return np_math::nm_pow(x, y);
 #else
   return rm_pow(x, y);
@@ -960,9 +1040,7 @@ __device__ __forceinline__ double k_pow(double x, double y) {
 // sin, cos, tan of a latitude (the RHS): the same values as k_sin/k_cos/k_tan
 __device__ __forceinline__ void k_sincostan(double x, double& s, double& c, double& t) {
 #if RWRT_MATH_NUMPY
-  s = np_math::nm_sin(x);
-  c = np_math::nm_cos(x);
-  t = np_math::nm_tan(x);
+  np_math::nm_sincostan(x, s, c, t);
 #elif RWRT_RHS_TRIG_SMALL
   // |lat| >= 2^30, inf or NaN: the ray is masked (|lat| >= pi/2) or its
   // lookup is NaN, so every output is NaN whatever s, c, tn are
@@ -1514,6 +1592,7 @@ __global__ void pack_fields_kernel(const double* __restrict__ ref, double* __res
 
 __global__ void mercator_kernel(Field F, int64_t n, const double* __restrict__ lon,
                                 const double* __restrict__ lat, double* __restrict__ out) {
+  nm_stage<NM_SINCOS | NM_TAN>();
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     const double la = lat[i];
@@ -1528,6 +1607,7 @@ __global__ void mercator_kernel(Field F, int64_t n, const double* __restrict__ l
 
 __global__ void rhs_kernel(Field F, int64_t n, const double* __restrict__ y,
                            double* __restrict__ dydt) {
+  nm_stage<NM_SINCOS | NM_TAN>();
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     double yy[5], d[5];
@@ -1543,6 +1623,7 @@ __global__ void attempt_kernel(Field F, int64_t n, const double* __restrict__ y,
                                const double* __restrict__ f, const double* __restrict__ h,
                                double rtol, double atol, double* __restrict__ Kout,
                                double* __restrict__ ynew, double* __restrict__ err) {
+  nm_stage<NM_SINCOS | NM_TAN>();
   const RayProblem P{StaticBG{F}};
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -1575,6 +1656,7 @@ struct InitArgs {
 
 template <class BG>
 __global__ void rk45_init_kernel(InitArgs<BG> a) {
+  nm_stage<NM_ALL>();
   const RayProblemT<BG> P{a.B};
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < a.nray;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -1661,6 +1743,7 @@ using KStore = KRegs<5>;
 #endif
 template <class BG>
 __global__ void __launch_bounds__(256, RWRT_WAVES_PER_SIMD) rk45_run_kernel(RunArgs<BG> a) {
+  nm_stage<NM_ALL>();
   using LBG = typename LaneBG<BG>::type;
   using RayProblem = RayProblemT<LBG>;
   // all LDS in one array: the stages (5 x 5 doubles per lane) then the lookup cache
@@ -1829,9 +1912,10 @@ __global__ void frozen_flag_kernel(const double* __restrict__ state, int64_t nra
 }
 
 // At most 128 VGPRs: a fill wave must fit beside the run kernel's wave in a
-// SIMD's register file (256 VGPRs + its AGPRs of 512), and its 8.7 KB of LDS
-// beside the run kernel's 146 KB, or the fill would wait for the run to end.
-constexpr int kFillThreads = 128;
+// SIMD's register file (256 VGPRs + its AGPRs of 512), and its LDS (4.4 KB of
+// row buffers + the 3.5 KB sin/cos table, one wave per block) beside the run
+// kernel's 151 KB, or the fill would wait for the run to end.
+constexpr int kFillThreads = 64;
 #ifndef RWRT_FILL_THROTTLE
 #define RWRT_FILL_THROTTLE 64
 #endif
@@ -1841,6 +1925,7 @@ constexpr int kFillThreads = 128;
 template <class BG>
 __global__ void __launch_bounds__(kFillThreads) __attribute__((amdgpu_num_vgpr(128)))
 frozen_fill_kernel(RunArgs<BG> a) {
+  nm_stage<NM_SINCOS>();
   __shared__ double2 rowbuf[kFillThreads][4];
   __shared__ int list[kFillThreads];
   __shared__ int cnt;
@@ -1907,6 +1992,7 @@ frozen_fill_kernel(RunArgs<BG> a) {
 
 __global__ void math_kernel(int kind, int64_t n, const double* __restrict__ x,
                             const double* __restrict__ y, double* __restrict__ out) {
+  nm_stage<NM_ALL>();
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (i >= n) return;
   const double a = x[i], b = y ? y[i] : 0.0;
@@ -1977,6 +2063,7 @@ struct Rk4Args {
 #define RWRT_RK4_CACHE 1   // the RHS lookups through rk45_run_kernel's per-lane LDS cell cache
 #endif
 __global__ void __launch_bounds__(256, RWRT_WAVES_PER_SIMD) rk4_run_kernel(Rk4Args a) {
+  nm_stage<NM_SINCOS | NM_TAN>();
   const int64_t nrows = a.it_end - a.it_begin;
 #if RWRT_RK4_CACHE
   __shared__ __attribute__((aligned(16))) char smem[LaneBG<StaticBG>::kLdsBytes];
@@ -2085,6 +2172,7 @@ __global__ void rk4_flag_kernel(const double* __restrict__ state, int64_t nray,
 
 __global__ void __launch_bounds__(kFillThreads) __attribute__((amdgpu_num_vgpr(128)))
 rk4_fill_kernel(Rk4Args a) {
+  nm_stage<NM_SINCOS>();
   __shared__ double2 rowbuf[kFillThreads][4];
   __shared__ int list[kFillThreads];
   __shared__ int cnt;
@@ -2147,6 +2235,7 @@ template <class P>
 __global__ void kat_kernel(int64_t ncol, const double* __restrict__ y0, int32_t nt,
                            const double* __restrict__ teval, double rtol, double atol,
                            double min_step, double* __restrict__ out) {
+  nm_stage<NM_ALL>();
   constexpr int NV = P::NV;
   const P fun{};
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
@@ -2628,6 +2717,7 @@ __global__ void ready_pack_kernel(ReadyArgs a) {
 template <class BG>
 __global__ void rhs_bg_kernel(BG B, int64_t n, const double* __restrict__ t,
                               const double* __restrict__ y, double* __restrict__ dydt) {
+  nm_stage<NM_SINCOS | NM_TAN>();
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     double yy[5], d[5];

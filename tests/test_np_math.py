@@ -42,6 +42,8 @@ def lib():
     P, I = ctypes.c_void_p, ctypes.c_int64
     for n in ("nm_sin_arr", "nm_cos_arr", "nm_tan_arr", "nm_rcp14_arr"):
         getattr(lib, n).argtypes = [P, P, I]
+    lib.nm_sincos_arr.argtypes = [P, P, P, I]
+    lib.nm_sincostan_arr.argtypes = [P, P, P, P, I]
     lib.nm_pow_arr.argtypes = [P, P, I, P, I]
     return lib
 
@@ -126,6 +128,30 @@ def test_pow_general_main_path(lib):
         xx, yy = np.meshgrid(sx, sy)
         assert_bitwise(power(lib, xx.ravel(), yy.ravel()), np.power(xx.ravel(), yy.ravel()),
                        xx.ravel(), "pow special values")
+
+
+def test_fused_sincos_is_sin_and_cos(lib):
+    """nm_sincos (one do_sin + one do_cos per lane, the kernels' RHS form) ==
+    np.sin and np.cos."""
+    x = trig_args(np.random.default_rng(4), 1 << 23)
+    s, c = np.empty_like(x), np.empty_like(x)
+    lib.nm_sincos_arr(x.ctypes.data, s.ctypes.data, c.ctypes.data, x.size)
+    with np.errstate(all="ignore"):
+        assert_bitwise(s, np.sin(x), x, "sincos: sin")
+        assert_bitwise(c, np.cos(x), x, "sincos: cos")
+
+
+def test_fused_sincostan_is_sin_cos_tan(lib):
+    """nm_sincostan (the RHS's latitude: one straight-line block, one
+    rare-argument branch) == np.sin, np.cos and np.tan."""
+    x = trig_args(np.random.default_rng(5), 1 << 22)
+    x = x[~(np.abs(x) > 65536.0)]
+    s, c, t = np.empty_like(x), np.empty_like(x), np.empty_like(x)
+    lib.nm_sincostan_arr(x.ctypes.data, s.ctypes.data, c.ctypes.data, t.ctypes.data, x.size)
+    with np.errstate(all="ignore"):
+        assert_bitwise(s, np.sin(x), x, "sincostan: sin")
+        assert_bitwise(c, np.cos(x), x, "sincostan: cos")
+        assert_bitwise(t, np.tan(x), x, "sincostan: tan")
 
 
 def test_rcp14_restatement(lib):

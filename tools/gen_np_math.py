@@ -12,9 +12,12 @@ GPU box's host computes with the same ones):
 * ``np.power``           -> SVML ``__svml_pow8_ha``: log2 / exp2 tables and
   polynomials;
 * ``VRCP14PD``           -> the host CPU's 14-bit reciprocal approximation
-  that both SVML routines start from: the result depends on the top 16
-  fraction bits of the input only (checked here), stored as 2-bit deltas of
-  consecutive 16-bit result mantissas.
+  that both SVML routines start from.  Probed on all 65536 mantissa buckets:
+  the result depends on the top 16 fraction bits i of the input only (checked
+  here), and its 16 fraction bits are exactly ``(A[k] - N[k] * o) >> 10``
+  with k = i >> 10, o = i & 1023 -- a 64-piece linear interpolation in fixed
+  point, whose integer knots are recovered here and checked against every
+  bucket (an exact power of two returns its exact reciprocal).
 
 The values are read from the shared objects themselves (file offset ==
 virtual address for their read-only segments) at the addresses their
@@ -62,7 +65,9 @@ def hexd(u):
     return f"0x{u:016X}ull"
 
 
-def rcp14_table():
+def rcp14_knots():
+    """The 64 (A, N) integer knots reproducing VRCP14PD's 16 result fraction
+    bits for every bucket, and the sha256 of the probe."""
     src = os.path.join(ROOT, "tools", "rcp14_probe.c")
     with tempfile.TemporaryDirectory() as d:
         exe, out = os.path.join(d, "p"), os.path.join(d, "t.bin")
@@ -75,9 +80,23 @@ def rcp14_table():
     assert np.all((t >> np.uint64(52)) == 0x3FE)           # (0.5, 1) otherwise
     assert np.all((t & np.uint64((1 << 36) - 1)) == 0)     # 16 fraction bits
     f = ((t >> np.uint64(36)) & np.uint64(0xFFFF)).astype(np.int64)
-    d = f[:-1] - f[1:]                                     # deltas from entry 0 on
-    assert d.min() >= 0 and d.max() <= 3
-    return int(f[0]), d, hashlib.sha256(both.tobytes()).hexdigest()
+    o = np.arange(1024, dtype=np.int64)
+    A, N = [], []
+    for k in range(64):
+        s = f[k * 1024:(k + 1) * 1024]
+        slope = (s[0] - s[-1]) * 1024 // 1023
+        for n in sorted(range(slope - 8, slope + 9), key=lambda v: abs(v - slope)):
+            lo, hi = np.max(1024 * s + n * o), np.min(1024 * s + 1023 + n * o)
+            if lo <= hi:
+                A.append(int(lo))
+                N.append(n)
+                break
+        else:
+            raise AssertionError(f"rcp14 segment {k} is not linear in fixed point")
+    A, N = np.array(A, np.int64), np.array(N, np.int64)
+    i = np.arange(65536)
+    assert np.array_equal((A[i >> 10] - N[i >> 10] * (i & 1023)) >> 10, f)   # every bucket
+    return A, N, hashlib.sha256(both.tobytes()).hexdigest()
 
 
 def main():
@@ -113,10 +132,7 @@ def main():
     log_lo = u64(npso, pb + 0x100, 32)
     exp_hi = u64(npso, pb + 0x200, 16)
     exp_lo = u64(npso, pb + 0x280, 16)
-    f1, deltas, sha = rcp14_table()
-    packed = np.zeros((len(deltas) + 15) // 16, np.uint32)
-    for i, d in enumerate(deltas):
-        packed[i // 16] |= np.uint32(int(d) << (2 * (i % 16)))
+    rA, rN, sha = rcp14_knots()
 
     lines = ["// GENERATED by tools/gen_np_math.py -- do not edit.",
              "// Constants and tables of the reference NumPy's transcendentals (see np_math.h):",
@@ -145,11 +161,12 @@ def main():
     arr("kP_LOG_LO", log_lo)
     arr("kP_EXP_HI", exp_hi)
     arr("kP_EXP_LO", exp_lo)
-    lines.append(f"NM_CONST unsigned kRCP14_F0 = {f1}u;   // 16-bit result fraction of entry 0")
-    arr("kRCP14_DELTA", packed, "unsigned", 8, lambda x: f"0x{x:08X}u")
+    lines.append("// VRCP14PD fraction bits of bucket i: (kRCP14_KNOT[2k] - kRCP14_KNOT[2k+1] * o) >> 10,")
+    lines.append("// k = i >> 10, o = i & 1023")
+    arr("kRCP14_KNOT", np.stack([rA, rN], 1).ravel(), "unsigned", 8, lambda x: f"{x}u")
     lines += ["", "}  // namespace np_math", ""]
     open(OUT, "w").write("\n".join(lines))
-    print("wrote", OUT, f"({len(deltas)} rcp14 deltas, sha {sha[:16]})")
+    print("wrote", OUT, f"(64 rcp14 knots, probe sha {sha[:16]})")
 
 
 if __name__ == "__main__":
