@@ -117,22 +117,35 @@ def cpu_baseline_mp(bg, y0, procs, rays_per_proc, days, seed=1):
     return steps, wall, len(pick)
 
 
+def library_sha():
+    """sha256 (16 hex digits) of the librwrt.so this process loaded: a
+    profile summary counts for this run only if it was taken on the same build."""
+    import hashlib
+    import _hip as H
+    return hashlib.sha256(open(H.LIB_PATH, "rb").read()).hexdigest()[:16]
+
+
 def find_profile(name, path, workload, schedule):
     """A per-launch profile summary (profiles/<round>/.../<name>) of this
-    workload run with the same launch schedule (rows per launch)."""
+    workload run with the same launch schedule (rows per launch), taken on
+    this build of the library if one is committed (else the newest, flagged)."""
     import glob
     # newest profile first by path (profiles/<round>/<version>/...: sorts the
     # same in any checkout, unlike file times)
     cands = [path] if path else sorted(glob.glob(os.path.join(ROOT, "profiles", "**", name), recursive=True),
                                        reverse=True)
+    sha, fallback = library_sha(), (None, None)
     for c in cands:
         try:
             t = json.load(open(c))
         except (OSError, ValueError):
             continue
         if t.get("workload") == workload and t.get("launch_rows") == schedule:
-            return t, os.path.relpath(c, ROOT)
-    return None, None
+            if t.get("library_sha256") == sha:
+                return t, os.path.relpath(c, ROOT)
+            if fallback[0] is None:
+                fallback = (dict(t, profile_of_other_build=True), os.path.relpath(c, ROOT))
+    return fallback
 
 
 def roofline(steps_per_launch, avg_launch_s, workload, schedule, bytes_per_step, args):
@@ -147,7 +160,8 @@ def roofline(steps_per_launch, avg_launch_s, workload, schedule, bytes_per_step,
     out = {"bound": "valu_issue", "achieved": None, "peak": None, "unit": "G VALU wave-instructions/s",
            "frac": None, "traffic": traffic["traffic_bytes_per_launch"] if traffic else None,
            "kernel": "rk45_run_kernel", "avg_launch_ms": 1e3 * avg_launch_s,
-           "valu_source": vsrc, "traffic_source": tsrc}
+           "valu_source": vsrc, "traffic_source": tsrc,
+           "profile_same_build": bool(valu) and not valu.get("profile_of_other_build", False)}
     if valu:
         ach = valu["valu_insts_per_launch"] / avg_launch_s
         peak = valu["simds"] * valu["clock_hz"] / valu["cycles_per_valu"]
@@ -329,6 +343,7 @@ def main():
             "init_bitwise_vs_host": init_same,
             "queue_order": args.order,
             "library": os.path.basename(os.environ.get("RWRT_LIB", "librwrt.so")),
+            "library_sha256": library_sha(),
             "roofline": roofline(per_launch_steps, avg_launch_s, workload, schedule, BYTES_PER_STEP, args),
         }
         if world == 1 and not args.no_cpu:
@@ -484,6 +499,7 @@ def main_c5(args, dist, group, rank, world, dev):
             "ray_steps_per_step": tot_steps / args.steps,
             "rejected_per_accepted": tot_rej * args.steps / max(tot_steps, 1),
             "levels_build_s": t_build,
+            "library_sha256": library_sha(),
             "init": "GPU rwrt_ray_initial inside every timed step",
             "roofline": roofline(per_launch_steps, avg_launch_s, workload, schedule, bps, args)}))
     if dist:

@@ -43,6 +43,7 @@ def main():
     steps_per_launch = bench["ray_steps_per_step"] / launches_per_step
     bps = bench["roofline"].get("bytes_per_ray_step") or bench["roofline"]["algorithmic"]["bytes_per_ray_step"]
     res = {"workload": bench["config"]["workload"], "launch_rows": bench["config"].get("launch_rows"),
+           "library_sha256": bench.get("library_sha256"),
            "kernel": "rk45_run_kernel", "kernels_summed": list(KERNELS), "launches": n,
            "fetch_bytes_per_launch_x2": 2 * fb, "write_bytes_per_launch": wb,
            "traffic_bytes_per_launch": 2 * fb + wb,

@@ -38,6 +38,7 @@ def main():
     clock = tot("GRBM_GUI_ACTIVE") / 8.0 / t
     insts = tot("SQ_INSTS_VALU") / n
     res = {"workload": bench["config"]["workload"], "launch_rows": bench["config"].get("launch_rows"),
+           "library_sha256": bench.get("library_sha256"),
            "kernel": KERNEL, "launches": n, "valu_insts_per_launch": insts,
            "clock_hz": clock, "simds": 1024, "cycles_per_valu": 4,
            "profiled_launch_ms": 1e3 * t / n,
