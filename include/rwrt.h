@@ -264,6 +264,18 @@ rwrt_status rwrt_kat_rk45(int32_t kind, int64_t ncol, const double* d_y0,
 rwrt_status rwrt_selftest_math(int32_t kind, int64_t n, const double* d_x,
                                const double* d_y, double* d_out, void* stream);
 
+/* HOST routine (no device call; the drop-in's delivery into the reference
+ * arrays, wr.py:868-876): rows [0, nrows) of a host block dst[nrows][ncol]
+ * (row stride ld doubles) become prev[ncol] -- the row before the block --
+ * except the nsrc columns cols[] (strictly ascending, < ncol), which take
+ * src[nrows][nsrc] (row stride ld_src).  A ray whose rows in a launch are all
+ * bitwise equal to its previous row (a frozen ray: rkf45.py:400-403) is then
+ * never shipped over PCIe; the block equals what a full copy would give, bit
+ * for bit.  Reentrant (callers split the rows over threads). */
+rwrt_status rwrt_host_fill_rows(double* dst, int64_t nrows, int64_t ncol, int64_t ld,
+                                const double* prev, const double* src, int64_t nsrc,
+                                int64_t ld_src, const int64_t* cols);
+
 #ifdef __cplusplus
 }
 #endif

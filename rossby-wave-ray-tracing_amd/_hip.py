@@ -18,7 +18,7 @@ ABI_SYMBOLS = ("rwrt_version", "rwrt_last_error", "rwrt_ctx_create", "rwrt_ctx_d
                "rwrt_mercator_point", "rwrt_rhs", "rwrt_dp54_attempt",
                "rwrt_ray_initial", "rwrt_rk45_init", "rwrt_rk45_run", "rwrt_rk4_run",
                "rwrt_bs_ready", "rwrt_rk45_init_tv", "rwrt_rk45_run_tv", "rwrt_rhs_tv",
-               "rwrt_kat_rk45", "rwrt_selftest_math")
+               "rwrt_kat_rk45", "rwrt_selftest_math", "rwrt_host_fill_rows")
 
 RWRT_OK, RWRT_ERR_ARG, RWRT_ERR_HIP, RWRT_SOLVER_FAILED = 0, 1, 2, 3
 
@@ -85,6 +85,7 @@ def load():
         "rwrt_rhs_tv": [G, B, _I64, _P, _P, _P, _P],
         "rwrt_kat_rk45": [_I32, _I64, _P, _I32, _P, _D, _D, _D, _P, _P],
         "rwrt_selftest_math": [_I32, _I64, _P, _P, _P, _P],
+        "rwrt_host_fill_rows": [_P, _I64, _I64, _I64, _P, _P, _I64, _I64, _P],
     }
     for name, args in sig.items():
         fn = getattr(lib, name)

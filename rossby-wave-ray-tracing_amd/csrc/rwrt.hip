@@ -3014,4 +3014,46 @@ rwrt_status rwrt_selftest_math(int32_t kind, int64_t n, const double* d_x, const
   return check_launch("math_kernel");
 }
 
+// Host side of the drop-in delivery (hostio.HistorySink): the block starts as
+// copies of the previous row, then the shipped columns are scattered in.
+rwrt_status rwrt_host_fill_rows(double* dst, int64_t nrows, int64_t ncol, int64_t ld,
+                                const double* prev, const double* src, int64_t nsrc,
+                                int64_t ld_src, const int64_t* cols) {
+  if (nrows < 0 || ncol < 0 || nsrc < 0 || nsrc > ncol || ld < ncol || ld_src < nsrc)
+    return fail(RWRT_ERR_ARG, "bad rwrt_host_fill_rows shape%s");
+  if (nrows == 0 || ncol == 0) return RWRT_OK;
+  if (!dst || (nsrc < ncol && !prev) || (nsrc > 0 && (!src || !cols)))
+    return fail(RWRT_ERR_ARG, "NULL buffer to rwrt_host_fill_rows%s");
+  for (int64_t j = 0; j < nsrc; ++j)
+    if (cols[j] < 0 || cols[j] >= ncol || (j > 0 && cols[j] <= cols[j - 1]))
+      return fail(RWRT_ERR_ARG, "cols must be strictly ascending in [0, ncol)%s");
+  typedef double v2d __attribute__((ext_vector_type(2)));
+  for (int64_t i = 0; i < nrows; ++i) {
+    double* d = dst + i * ld;
+    const double* s = src + i * ld_src;
+    if (nsrc == ncol) {
+      std::memcpy(d, s, sizeof(double) * ncol);
+      continue;
+    }
+    // Each 64-B line of the row is assembled from the previous row and the
+    // shipped columns that fall in it, then written with non-temporal stores
+    // (the block is far larger than the caches: no read-for-ownership).
+    int64_t j = 0, c = 0;
+    for (; c < ncol && (reinterpret_cast<uintptr_t>(d + c) & 63); ++c)
+      d[c] = (j < nsrc && cols[j] == c) ? s[j++] : prev[c];
+    for (; c + 8 <= ncol; c += 8) {
+      double line[8];
+      std::memcpy(line, prev + c, sizeof(line));
+      for (; j < nsrc && cols[j] < c + 8; ++j) line[cols[j] - c] = s[j];
+      for (int q = 0; q < 8; q += 2) {
+        const v2d v = {line[q], line[q + 1]};
+        __builtin_nontemporal_store(v, reinterpret_cast<v2d*>(d + c + q));
+      }
+    }
+    for (; c < ncol; ++c) d[c] = (j < nsrc && cols[j] == c) ? s[j++] : prev[c];
+  }
+  __builtin_ia32_sfence();   // the streaming stores are visible before the caller's release
+  return RWRT_OK;
+}
+
 }  // extern "C"

@@ -4,91 +4,182 @@
 fp64 each, ``wr.py:160-167, 868-876``) row by row.  The GPU path produces
 rows in chunks of ``[nray][rows][8]`` (``engine.RayEngine.integrate``);
 ``HistorySink`` moves each chunk into those arrays while the GPU already
-integrates the next one:
+integrates the next one, and ships over PCIe only the rays whose rows
+changed:
 
-  compute stream   launch k ──────────── launch k+1 ─────────── launch k+2
-  copy stream        └─ permute(k) → D2H(k) into pinned staging
-  host threads                         └─ 7 memcpys into rlon..rvg [i0:i1]
+  compute stream  launch k ───────────── launch k+1 ──────────── launch k+2
+  copy stream       └ compare(k)  ┌ gather(k) → D2H(k) into pinned staging
+  host threads                    │            └ rwrt_host_fill_rows(k)
+  main thread     (after launch k+1 is queued) ┘ nonzero(changed k)
 
-* two device row buffers alternate (``buffers()``); launch k+2 waits for the
-  permute of chunk k before it overwrites that buffer;
-* the permute to ``[7][rows][nray]`` (the reference layout per variable) runs
-  on the device; the D2H goes into page-locked staging (DMA at PCIe rate);
-* the host copies run in a thread pool (NumPy releases the GIL for them);
-  staging buffer b is reused only after chunk k-2's copies finished.
+* ``compare(k)``: a ray is *changed* in chunk k when any of its 7 delivered
+  values in any row differs, bit for bit, from its previous row (kept on the
+  device, starting from the host's row 0).  Frozen rays (``rkf45.py:400-403``:
+  dead root slots, rays masked earlier -- 70 % of C3's slots) repeat their
+  last row forever, so after the first chunk they are never shipped;
+* ``gather(k)``: the changed rays' rows, permuted on the device to the
+  reference layout ``[7][rows][nchanged]``, then one D2H into page-locked
+  staging;
+* ``rwrt_host_fill_rows`` (C ABI, host code, GIL released) writes each row
+  block of each variable: every column a copy of the previous row (shipped
+  with the chunk, 7 x nray doubles, so no chunk's host work waits for
+  another's), the shipped columns scattered in -- exactly what copying the
+  whole chunk would write;
+* two device row buffers alternate (``buffers()``): launch k+2 waits for
+  ``gather(k)`` before it overwrites buffer k % 2.
 
 ``finish()`` waits for everything; afterwards the arrays hold exactly the
 rows the device produced (tests/test_gpu_parity.py::test_dropin_history_*).
 """
+import threading
+import time
 from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 import torch
 
+import _hip as H
+
 F64 = torch.float64
 _PINNED = {}
 
 
-def _pinned(shape):
-    """Two page-locked staging buffers, kept across runs (pinning is slow)."""
-    key = tuple(shape)
-    if key not in _PINNED:
+def _pinned(n):
+    """Two page-locked staging buffers of ``n`` doubles, kept across runs
+    (pinning is slow)."""
+    if n not in _PINNED:
         _PINNED.clear()
-        _PINNED[key] = [torch.empty(key, dtype=F64, pin_memory=True) for _ in range(2)]
-    return _PINNED[key]
+        _PINNED[n] = [torch.empty(n, dtype=F64, pin_memory=True) for _ in range(2)]
+    return _PINNED[n]
+
+
+def fill_rows(dst, prev, src, cols):
+    """``dst[r, ncol]`` (a C-contiguous host block) := ``prev`` in every column
+    except ``cols`` (ascending int64), which take ``src[r, len(cols)]``."""
+    r, ncol = dst.shape
+    n = 0 if cols is None else len(cols)
+    H.check(H.load().rwrt_host_fill_rows(
+        dst.ctypes.data, r, ncol, dst.strides[0] // 8,
+        None if prev is None else prev.ctypes.data,
+        None if n == 0 else src.ctypes.data, n, src.strides[0] // 8 if n else 0,
+        None if n == 0 else cols.ctypes.data))
 
 
 class HistorySink:
-    def __init__(self, hist, rows_shape, nray, max_rows, device, progress=None, workers=8):
+    def __init__(self, hist, rows_shape, nray, max_rows, device, progress=None, workers=16):
+        if not all(h.flags.c_contiguous and h.dtype == np.float64 for h in hist):
+            raise ValueError("the history arrays must be C-contiguous float64 (wr.py:160-167)")
         self.hist, self.rows_shape, self.nray = hist, rows_shape, nray
         self.progress = progress
         self.device = device
+        self.workers = workers
         self.copy_stream = torch.cuda.Stream(device=device)
-        self.stage_dev = [torch.empty((7, max_rows, nray), dtype=F64, device=device) for _ in range(2)]
-        self.stage_host = _pinned((7, max_rows, nray))
+        self.stage_dev = [torch.empty(7 * max_rows * nray, dtype=F64, device=device) for _ in range(2)]
+        self.stage_host = _pinned(7 * max_rows * nray)
         self.out = [torch.empty((nray, max_rows, 8), dtype=F64, device=device) for _ in range(2)]
+        # row 0 (the host initial rows) is every ray's "previous row" of chunk 1
+        row0 = np.stack([np.ascontiguousarray(h[0]).reshape(-1) for h in hist], axis=1)
+        self.last = torch.as_tensor(row0).to(device).view(torch.int64)       # [nray, 7] bits
+        self.changed = [torch.empty(nray, dtype=torch.bool, device=device) for _ in range(2)]
+        # each chunk's previous row travels with it (7 x nray doubles): the
+        # host fill of a chunk then depends on no other chunk's
+        self.prev_dev = [torch.empty((7, nray), dtype=F64, device=device) for _ in range(2)]
+        self.prev_host = [torch.empty((7, nray), dtype=F64, pin_memory=True) for _ in range(2)]
         self.pool = ThreadPoolExecutor(max_workers=workers)
         self.futs = [[], []]
-        self.perm_done = [None, None]
+        self.pending = None
+        self.gathered = [None, None]
         self.k = 0
+        self.lock = threading.Lock()
+        self.t_wait = self.t_fill = 0.0   # summed over tasks (diagnostic)
+        self.shipped = 0          # rays x rows shipped over PCIe (diagnostic)
+        self.delivered = 0
 
     def buffers(self):
         """The two device row buffers the engine alternates between."""
         return self.out
 
-    def _copy_rows(self, ev, b, v, i0, i1):
-        ev.synchronize()
-        r = i1 - i0
-        src = self.stage_host[b].numpy()[v, :r]
-        self.hist[v][i0:i1] = src.reshape((r,) + self.rows_shape)
-
     def __call__(self, i0, i1, view):
         k, b = self.k, self.k % 2
         self.k += 1
-        r = i1 - i0
-        # launch k+1 writes the buffer chunk k-1 was read from
-        if self.perm_done[1 - b] is not None:
-            torch.cuda.current_stream(self.device).wait_event(self.perm_done[1 - b])
-        # staging b was last used by chunk k-2
-        for f in self.futs[b]:
-            f.result()
+        # the previous chunk first: its nonzero() waits for its compare only
+        # (this launch is already queued, so the GPU stays busy meanwhile)
+        if self.pending is not None:
+            self._flush(*self.pending)
+            self.pending = None
         ready = torch.cuda.Event()
         ready.record(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(self.copy_stream):
             self.copy_stream.wait_event(ready)
-            dst = self.stage_dev[b][:, :r]
-            dst.copy_(view[:, :, :7].permute(2, 1, 0))
-            perm = torch.cuda.Event()
-            perm.record(self.copy_stream)
-            self.stage_host[b][:, :r].copy_(dst, non_blocking=True)
-            d2h = torch.cuda.Event()
-            d2h.record(self.copy_stream)
-        self.perm_done[b] = perm
-        self.futs[b] = [self.pool.submit(self._copy_rows, d2h, b, v, i0, i1) for v in range(7)]
+            bits = view[:, :, :7].view(torch.int64)
+            self.prev_dev[b].copy_(self.last.t().view(F64))
+            torch.any((bits != self.last[:, None, :]).reshape(self.nray, -1), dim=1, out=self.changed[b])
+            self.last.copy_(bits[:, -1, :])
+        self.pending = (b, i0, i1, view)
+        # launch k+1 writes the buffer chunk k-1 was read from: its gather
+        # was queued by the _flush above
+        if self.gathered[1 - b] is not None:
+            torch.cuda.current_stream(self.device).wait_event(self.gathered[1 - b])
         if self.progress is not None:
             self.progress(i1 - 1)
 
+    def _flush(self, b, i0, i1, view):
+        r = i1 - i0
+        # staging b and prev_host b were last read by chunk k-2's host tasks
+        for f in self.futs[b]:
+            f.result()
+        with torch.cuda.stream(self.copy_stream):
+            self.prev_host[b].copy_(self.prev_dev[b], non_blocking=True)
+            cols = torch.nonzero(self.changed[b]).squeeze(1)     # syncs on this chunk's compare
+            n = int(cols.numel())
+            stage = self.stage_dev[b][: 7 * r * n].view(7, r, n)
+            if n == self.nray:
+                stage.copy_(view[:, :, :7].permute(2, 1, 0))
+            elif n:
+                stage.copy_(view.index_select(0, cols)[:, :, :7].permute(2, 1, 0))
+            g = torch.cuda.Event()
+            g.record(self.copy_stream)
+            cols_h = cols.cpu().numpy() if 0 < n < self.nray else None
+            host = self.stage_host[b][: 7 * r * n]
+            d2h = []                 # one DMA per variable: its host fill starts when it lands
+            for v in range(7):
+                if n:
+                    host[v * r * n:(v + 1) * r * n].copy_(stage[v].view(-1), non_blocking=True)
+                d2h.append(torch.cuda.Event())
+                d2h[-1].record(self.copy_stream)
+        self.gathered[b] = g
+        self.shipped += n * r
+        self.delivered += self.nray * r
+        src = host.numpy().reshape(7, r, n)
+        prev = self.prev_host[b].numpy()
+        step = max(1, -(-r * 7 // self.workers))
+        self.futs[b] = [self.pool.submit(self._fill, d2h[v], src, prev[v], v, a, min(a + step, r), i0,
+                                         cols_h)
+                        for v in range(7) for a in range(0, r, step)]
+
+    def _fill(self, ev, src, prev, v, a, e, i0, cols):
+        t0 = time.perf_counter()
+        ev.synchronize()
+        t1 = time.perf_counter()
+        self._fill_rows(src, prev, v, a, e, i0, cols)
+        t2 = time.perf_counter()
+        with self.lock:
+            self.t_wait += t1 - t0
+            self.t_fill += t2 - t1
+
+    def _fill_rows(self, src, prev, v, a, e, i0, cols):
+        h = self.hist[v]
+        dst = h[i0 + a:i0 + e].reshape(e - a, self.nray)
+        n = src.shape[2]
+        if n == self.nray:
+            dst[:] = src[v, a:e]
+            return
+        fill_rows(dst, prev, src[v, a:e], cols)
+
     def finish(self):
+        if self.pending is not None:
+            self._flush(*self.pending)
+            self.pending = None
         for fs in self.futs:
             for f in fs:
                 f.result()

@@ -210,6 +210,9 @@ class WR:
         finally:
             if hs is not None:
                 hs.finish()
+                # ray-rows shipped over PCIe vs delivered (frozen rays' rows are filled on the host)
+                self.last_delivery = {"shipped_ray_rows": hs.shipped, "delivered_ray_rows": hs.delivered,
+                                      "host_fill_s": hs.t_fill, "host_wait_s": hs.t_wait}
         if res.break_row is not None:
             for h in hist:
                 h[res.break_row:] = np.nan     # rows never stored (wr.py:853-855, 886-887)

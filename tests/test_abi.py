@@ -55,3 +55,33 @@ def test_context_needs_a_device():
     assert lib.rwrt_ctx_create(4096, ctypes.byref(h)) == H.RWRT_ERR_ARG
     assert not h.value
     assert lib.rwrt_ctx_destroy(None) == H.RWRT_OK
+
+
+def test_host_fill_rows():
+    """rwrt_host_fill_rows (host code, no GPU): the drop-in's row delivery
+    equals copying the whole block, for scattered, edge, empty and full
+    column sets; bad column lists are refused."""
+    import numpy as np
+    from hostio import fill_rows
+    rng = np.random.default_rng(0)
+    ncol, r = 1000, 9
+    prev = rng.standard_normal(ncol)
+    for cols in (np.array([], np.int64), np.array([0], np.int64), np.array([ncol - 1], np.int64),
+                 np.array([0, 1, 2, 500, 998, 999], np.int64),
+                 np.sort(rng.choice(ncol, 300, replace=False)).astype(np.int64),
+                 np.arange(ncol, dtype=np.int64)):
+        src = rng.standard_normal((r, len(cols)))
+        want = np.tile(prev, (r, 1))
+        want[:, cols] = src
+        block = np.full((r + 2, ncol), np.nan)
+        dst = block[1:1 + r]
+        fill_rows(dst, prev, src, cols if len(cols) else None)
+        assert np.array_equal(dst, want)
+        assert np.isnan(block[0]).all() and np.isnan(block[-1]).all()
+    lib = H.load()
+    bad = np.array([3, 3], np.int64)
+    dst = np.zeros((2, 10))
+    src = np.zeros((2, 2))
+    st = lib.rwrt_host_fill_rows(dst.ctypes.data, 2, 10, 10, prev.ctypes.data, src.ctypes.data, 2, 2,
+                                 bad.ctypes.data)
+    assert st == H.RWRT_ERR_ARG and b"ascending" in lib.rwrt_last_error()

@@ -371,6 +371,39 @@ def test_rk4_c1_90d_bitwise():
 
 
 # ------------------------------------------------------------ drop-in delivery
+def test_history_sink_delivers_bitwise():
+    """hostio.HistorySink on synthetic chunks (rays that change, rays frozen
+    from a row on -- NaN payloads of either sign included -- and a chunk where
+    nothing changes): the host arrays equal the device rows bit for bit, and
+    only changed rays were shipped."""
+    from hostio import HistorySink
+    rng = np.random.default_rng(5)
+    nray, nt, rows_shape = 500, 30, (5, 100)
+    full = rng.standard_normal((nray, nt, 8))
+    freeze = rng.integers(1, nt + 8, nray)            # row from which a ray repeats itself
+    for i in range(nray):
+        if freeze[i] < nt:
+            full[i, freeze[i]:] = full[i, freeze[i]]
+    neg_nan = np.frombuffer(np.uint64(0xFFF8000000000001).tobytes(), np.float64)[0]
+    full[::7, 3:, 3] = neg_nan                        # frozen NaN with a payload
+    full[:, 20:25] = full[:, 19:20]                   # chunk [20, 25): every ray repeats row 19
+    hist = tuple(np.full((nt,) + rows_shape, np.nan) for _ in range(7))
+    for v in range(7):
+        hist[v][0] = full[:, 0, v].reshape(rows_shape)
+    sink = HistorySink(hist, rows_shape, nray, 8, torch.device("cuda"))
+    bufs = sink.buffers()
+    for k, (i0, i1) in enumerate([(1, 5), (5, 13), (13, 20), (20, 25), (25, 30)]):
+        view = bufs[k % 2].view(-1)[: nray * (i1 - i0) * 8].view(nray, i1 - i0, 8)
+        torch.cuda.current_stream().synchronize()
+        view.copy_(torch.as_tensor(full[:, i0:i1]))
+        sink(i0, i1, view)
+    sink.finish()
+    got = np.stack([h.reshape(nt, nray) for h in hist], axis=2)       # [nt, nray, 7]
+    want = np.transpose(full[:, :, :7], (1, 0, 2))
+    assert np.array_equal(got.view(np.int64), want.view(np.int64))
+    assert sink.shipped < sink.delivered == (nt - 1) * nray
+
+
 @pytest.mark.parametrize("inte_method", ["rk45", ""])
 def test_dropin_history_matches_engine_rows(inte_method):
     """WR.ray_run(mode='hip') delivers every chunk into rlon..rvg through
@@ -402,3 +435,6 @@ def test_dropin_history_matches_engine_rows(inte_method):
     a, b = got[:, 1:], want
     assert np.array_equal(np.where(np.isnan(a), np.nan, a).view(np.int64),
                           np.where(np.isnan(b), np.nan, b).view(np.int64))
+    # frozen rays (NaN-root slots, rays masked on the way) were filled on the host
+    d = w.last_delivery
+    assert 0 < d["shipped_ray_rows"] < d["delivered_ray_rows"] == (nt - 1) * y0.shape[1]

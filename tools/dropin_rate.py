@@ -60,7 +60,8 @@ def main():
                       "slots": int(y0.shape[1]), "ray_steps": steps, "history_bytes": int(nbytes),
                       "dropin_s": wall, "dropin_rate": steps / wall,
                       "device_only_s": kern, "device_only_rate": steps / kern,
-                      "launch_rows": [b - a_ for a_, b in res.bounds]}))
+                      "launch_rows": [b - a_ for a_, b in res.bounds],
+                      "delivery": getattr(w, "last_delivery", None)}))
 
 
 if __name__ == "__main__":
