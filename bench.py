@@ -209,7 +209,8 @@ def main():
                          "0.25-degree time-varying background)")
     ap.add_argument("--fields", default="fp64", choices=["fp64", "fp32"],
                     help="C5: storage of the background levels (arithmetic is fp64 either way)")
-    ap.add_argument("--c5-periods", type=int, default=2, help="C5 periods (1-5 of the C3 list)")
+    ap.add_argument("--c5-periods", type=int, default=5,
+                    help="C5 periods (1-5 of the C3 list; 5 = 9.67 M slots, ~4 M live rays: BASELINE's size)")
     ap.add_argument("--lib", default=None, help="alternative librwrt build (A/B timing)")
     ap.add_argument("--traffic", default=None, help="traffic.json (tools/pmc_traffic.py)")
     ap.add_argument("--valu-profile", default=None, help="valu.json (tools/pmc_valu.py)")

@@ -13,6 +13,8 @@ crosses ranks is setup and collection only:
   (solver failure, rkf45.py:423-425; early exit, wr.py:853-855) evaluated over
   all ranks so that a sharded run equals the single-GPU run exactly;
 * ``gather_rows``     -- per-chunk trajectory rows back to rank 0;
+* ``gather_changed_rows`` -- the same for the drop-in, but only the rays whose
+  rows changed (frozen rays repeat their previous row: ~70 % of C3's slots);
 * ``cost_partition`` / ``run_sharded`` -- BASELINE configs[3] (C4): ONE ray set
   split over the ranks by measured cost (a short probe launch over every ray,
   then a longest-first snake deal), each rank integrating its shard, the
@@ -123,6 +125,49 @@ def gather_rows(local, idx, nray, dst=0, group=None):
     for s, b, ib in zip(sizes, bufs, ibufs):
         out[ib[:s]] = b[:s]
     return out
+
+
+def gather_changed_rows(local, idx, last, dst=0, group=None):
+    """The multi-rank drop-in's per-chunk collection: only rays whose rows changed.
+
+    ``local[n_local, rows, >= 7]`` are this rank's rows of a chunk (rays
+    ``idx``, a device or host int64 tensor); ``last[n_local, 7]`` (int64 bit
+    patterns, updated in place) each ray's previous row.  A ray is sent when
+    any of its 7 delivered values in any row differs bit for bit from its
+    previous row -- a frozen ray (rkf45.py:400-403) repeats itself and is
+    never sent again.  Returns ``(cols, rows)`` on ``dst`` -- the changed
+    rays' global indices, ascending, and their rows ``[n, rows, 7]`` -- and
+    ``None`` elsewhere; the receiver copies every other ray's previous row
+    (hostio.fill_rows).
+    """
+    rank, world = world_info(group)
+    bits = local[:, :, :7].contiguous().view(torch.int64)
+    changed = torch.any((bits != last[:, None, :]).reshape(bits.shape[0], -1), dim=1)
+    last.copy_(bits[:, -1, :])
+    sel = torch.nonzero(changed).squeeze(1)
+    rows = bits.index_select(0, sel)
+    gidx = torch.as_tensor(idx, device=local.device)[sel]
+    if world > 1:
+        dev = _dev(group)
+        n = torch.tensor([int(sel.numel())], dtype=torch.int64, device=dev)
+        sizes = [torch.zeros_like(n) for _ in range(world)]
+        dist.all_gather(sizes, n, group=group)
+        sizes = [int(x) for x in sizes]
+        m = max(sizes)
+        pad = torch.zeros((m,) + tuple(rows.shape[1:]), dtype=torch.int64, device=dev)
+        pad[: rows.shape[0]] = rows.to(dev)
+        ipad = torch.full((m,), -1, dtype=torch.int64, device=dev)
+        ipad[: gidx.numel()] = gidx.to(dev)
+        bufs = [torch.empty_like(pad) for _ in range(world)] if rank == dst else None
+        ibufs = [torch.empty_like(ipad) for _ in range(world)] if rank == dst else None
+        dist.gather(pad, bufs, dst=dst, group=group)
+        dist.gather(ipad, ibufs, dst=dst, group=group)
+        if rank != dst:
+            return None
+        rows = torch.cat([b[:k] for k, b in zip(sizes, bufs)])
+        gidx = torch.cat([b[:k] for k, b in zip(sizes, ibufs)])
+    order = torch.argsort(gidx)
+    return gidx[order], rows[order].view(torch.float64)
 
 
 def cost_partition(cost, frozen, rank, world):

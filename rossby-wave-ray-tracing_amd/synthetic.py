@@ -125,7 +125,7 @@ CONFIGS = {
     "C3": dict(SW_lon=0.0, SW_lat=-88.0, dlon=2, dlat=2, nnx=180, nny=89,
                zwn=[float(k) for k in range(1, 11)]),
     # C5 (BASELINE configs[4]): 1-degree global seeds x k = 1..10 on the 0.25-degree
-    # time-varying background; x 2 periods {stationary, 10 d} = 3.87 M ray slots
+    # time-varying background; x the 5 C3 periods = 9.67 M ray slots (~4 M live)
     "C5": dict(SW_lon=0.0, SW_lat=-89.0, dlon=1, dlat=1, nnx=360, nny=179,
                zwn=[float(k) for k in range(1, 11)]),
 }

@@ -176,14 +176,24 @@ class WR:
         rows_shape = (3, self.nsource, self.nzwn)
         hist = (self.rlon, self.rlat, self.rzwn, self.rmwn, self.ramp, self.rug, self.rvg)
 
+        if world > 1:
+            # each rank's previous rows (row 0: the initial rows), as bit patterns
+            row0 = np.stack([h[0].reshape(-1)[idx] for h in hist], axis=1)
+            last = torch.as_tensor(np.ascontiguousarray(row0)).view(torch.int64).to(eng.device)
+
         def sink(i0, i1, rows):
-            if world > 1:
-                rows = shard.gather_rows(rows, idx, nray, 0, group)
-                if rows is None:
-                    return
-            host = rows[:, :, :7].permute(2, 1, 0).contiguous().cpu().numpy()
+            # rank 0 receives only the rays whose rows changed; every other
+            # ray repeats its previous row (hostio.fill_rows)
+            got = shard.gather_changed_rows(rows, torch.as_tensor(idx, device=rows.device), last, 0, group)
+            if got is None:
+                return
+            cols, data = got
+            host = data.permute(2, 1, 0).contiguous().cpu().numpy()        # [7][rows][n]
+            cols = np.ascontiguousarray(cols.cpu().numpy())
+            from hostio import fill_rows
             for v in range(7):
-                hist[v][i0:i1] = host[v].reshape((i1 - i0,) + rows_shape)
+                dst = hist[v][i0:i1].reshape(i1 - i0, nray)
+                fill_rows(dst, hist[v][i0 - 1].reshape(nray), host[v], cols if len(cols) else None)
             if self.progress:
                 progress_bar(i1 - 1, self.nt)
 

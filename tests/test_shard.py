@@ -106,3 +106,62 @@ def test_cost_partition_is_a_balanced_split(world):
     assert len(owners) == world
     # the same rule on every rank: repeated evaluation is identical
     assert all(torch.equal(shard.cost_partition(cost, frozen, r, world), parts[r]) for r in range(world))
+
+
+def _delta_worker(rank, world, port, q):
+    """Each rank sends only its changed rays per chunk (shard.gather_changed_rows);
+    rank 0 rebuilds the full history with hostio.fill_rows."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import shard
+        from hostio import fill_rows
+        rng = np.random.default_rng(3)
+        nray, nt = 203, 25
+        full = rng.standard_normal((nray, nt, 8))          # the same on every rank
+        freeze = rng.integers(1, nt + 5, nray)
+        for i in range(nray):
+            if freeze[i] < nt:
+                full[i, freeze[i]:] = full[i, freeze[i]]
+        full[::5, 4:, 2] = np.nan
+        full[:, 12:18] = full[:, 11:12]                     # a chunk where nothing changes
+        idx = shard.shard_indices(np.ones(nray, bool), rank, world)
+        last = torch.as_tensor(np.ascontiguousarray(full[idx, 0, :7])).view(torch.int64).clone()
+        hist = np.full((nt, nray, 7), np.nan)
+        hist[0] = full[:, 0, :7]
+        sent = 0
+        for i0, i1 in [(1, 6), (6, 12), (12, 18), (18, 25)]:
+            local = torch.as_tensor(np.ascontiguousarray(full[idx, i0:i1]))
+            got = shard.gather_changed_rows(local, torch.as_tensor(idx), last, 0)
+            if rank == 0:
+                cols, data = got
+                sent += cols.numel()
+                host = data.permute(2, 1, 0).contiguous().numpy()
+                c = np.ascontiguousarray(cols.numpy())
+                for v in range(7):
+                    blk = np.empty((i1 - i0, nray))
+                    fill_rows(blk, np.ascontiguousarray(hist[i0 - 1, :, v]), host[v], c if len(c) else None)
+                    hist[i0:i1, :, v] = blk
+        if rank == 0:
+            q.put(("ok", hist, np.transpose(full[:, :, :7], (1, 0, 2)), sent))
+    except Exception as e:  # pragma: no cover
+        q.put(("err", repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_world2_gloo_changed_rows_gather():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_delta_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+    assert res[0] == "ok", res
+    _, hist, want, sent = res
+    assert np.array_equal(hist.view(np.int64), want.view(np.int64))   # bit for bit
+    assert sent < 4 * 203                                             # frozen rays were not sent
