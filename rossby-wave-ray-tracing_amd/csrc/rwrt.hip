@@ -20,6 +20,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <type_traits>
 
 #include "rwrt.h"
 #include "nproots.h"
@@ -473,6 +474,31 @@ __device__ __forceinline__ char* lds_slice_base(char* wave_base) {
 // that carry scopes too -- which these (through lds_slice_base) do not.
 __device__ __forceinline__ void lds_dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
+// Timing-only diagnostic build (RWRT_DIAG_STAMPS=1, tools/stamps.py): cycle
+// counts of the sections of an attempt, summed over the active lanes' waves
+// (one count per wave, from its first active lane: per-wave time, for a
+// single ray or a whole batch).  RWRT_STAMP(k) charges the cycles since the
+// previous stamp of the wave to section k.
+#ifndef RWRT_DIAG_STAMPS
+#define RWRT_DIAG_STAMPS 0
+#endif
+#if RWRT_DIAG_STAMPS
+__device__ unsigned long long g_stamp[16];
+__shared__ unsigned long long s_stamp_last[4];   // per wave of the block
+#define RWRT_STAMP(k)                                                        \
+  do {                                                                       \
+    const unsigned long long _t = __builtin_amdgcn_s_memtime();             \
+    const unsigned _w = (threadIdx.x >> 6) & 3;                              \
+    if (__lane_id() == __builtin_amdgcn_readfirstlane(__lane_id()))          \
+      atomicAdd(&g_stamp[k], _t - s_stamp_last[_w]);                         \
+    s_stamp_last[_w] = _t;                                                   \
+  } while (0)
+#else
+#define RWRT_STAMP(k) \
+  do {                \
+  } while (0)
+#endif
+
 struct CachedStaticBG {
   static constexpr bool kTimeVarying = false;
   Field F;
@@ -489,6 +515,10 @@ struct CachedStaticBG {
   __device__ __forceinline__ Pending begin(double lon, double lat) const {
     const Corners k = corners(F, py_mod_2pi(lon), lat);
     if (k.key_x != key_x || k.key_y != key_y) {   // miss: refill the slice by LDS-DMA
+#if RWRT_DIAG_STAMPS
+      RWRT_STAMP(1);
+      if (__lane_id() == __builtin_amdgcn_readfirstlane(__lane_id())) atomicAdd(&g_stamp[11], 1ull);
+#endif
       const double* src[4] = {k.a, k.b, k.c, k.d};
       char* const base = lds_slice_base(wave_base);
 #pragma unroll
@@ -499,11 +529,14 @@ struct CachedStaticBG {
                                            (lds_void_ptr)(base + (j * 6 + q) * 1024), 16, 0, 0);
       key_x = k.key_x;
       key_y = k.key_y;
+      RWRT_STAMP(10);
     }
     return Pending{k.wa, k.wb, k.wc, k.wd};
   }
   __device__ __forceinline__ void end(const Pending& p, double g[11]) const {
+    RWRT_STAMP(2);
     lds_dma_wait();
+    RWRT_STAMP(12);
     Corners k;
     k.wa = p.wa;
     k.wb = p.wb;
@@ -1136,9 +1169,11 @@ __device__ __forceinline__ void ray_rhs(const BG& B, double t, const double* y, 
   const bool bad = fabs(lat) >= kHalfPi || fabs(y[3]) >= 100.0;
   const double ky = bad ? kNaN : y[3], amp = y[4];
   double g[11];
+  RWRT_STAMP(0);
 #if !RWRT_DIAG_NOINTERP
   const auto pending = lookup_begin(B, lon, lat, t);   // the lookup's fill overlaps the trig
 #endif
+  RWRT_STAMP(1);
   double s, c;
 #if RWRT_DIAG_NOTRIG     // timing-only diagnostic build: polynomial stand-ins
   s = lat * (1.0 - lat * lat * (1.0 / 6.0));
@@ -1148,6 +1183,7 @@ __device__ __forceinline__ void ray_rhs(const BG& B, double t, const double* y, 
   double tn;
   k_sincostan(lat, s, c, tn);       // np.cos, np.sin, np.tan of lat (bs.py:856-880)
 #endif
+  RWRT_STAMP(2);
 #if RWRT_DIAG_NOINTERP   // timing-only diagnostic build: constant background
 #pragma unroll
   for (int q = 0; q < 11; ++q) g[q] = 1e-5 * (q + 1) + 1e-9 * lat;
@@ -1155,9 +1191,11 @@ __device__ __forceinline__ void ray_rhs(const BG& B, double t, const double* y, 
   __builtin_amdgcn_sched_barrier(0);
   lookup_end(B, pending, g);
 #endif
+  RWRT_STAMP(3);
   const Merc M = merc_factors(lat, c, s);
   double o[12];
   mercator12(g, M, tn, o);
+  RWRT_STAMP(4);
   const double fmu = o[0], fmv = o[1], fmux = o[2], fmuy = o[3], fmvx = o[4], fmvy = o[5];
   const double fmqx = o[6], fmqy = o[7], fmqxx = o[8], fmqxy = o[9], fmqyx = o[10], fmqyy = o[11];
   double ug, vg;
@@ -1179,6 +1217,7 @@ __device__ __forceinline__ void ray_rhs(const BG& B, double t, const double* y, 
   div2(ug, kREarth, vg * c, kREarth, dy[0], dy[1]);     // x / R, x / R
   div2(dzwn, kREarth, dmwn, kREarth, dy[2], dy[3]);
   dy[4] = div_rearth(damp * amp);
+  RWRT_STAMP(5);
   if (aux) {
     aux[0] = ug;
     aux[1] = vg;
@@ -1390,6 +1429,13 @@ __device__ __forceinline__ double stage_input(const KS& K, double t, const doubl
   return t + kCs[S] * h;
 }
 
+// A problem whose RHS is evaluated by a whole block (rk45_team_kernel) says so
+// with kTeam = true and a stage(s, t, y, dy) member.
+template <class P, class = void>
+struct IsTeam : std::false_type {};
+template <class P>
+struct IsTeam<P, std::void_t<decltype(P::kTeam)>> : std::bool_constant<P::kTeam> {};
+
 // One DP5(4) attempt: rk_step (rkf45.py:259-321) + _estimate_error_norm
 // (rkf45.py:368-373).  The six stage evaluations are unrolled (six inlined RHS
 // copies, ~45 KB of code: fits the instruction cache; RWRT_UNROLL_STAGES=0
@@ -1422,7 +1468,8 @@ __device__ __forceinline__ double dp54_attempt(const P& fun, KS& K, double t, co
       case 5: ts = stage_input<5, NV>(K, t, y, f, h, ys); break;
       default: ts = stage_input<6, NV>(K, t, y, f, h, ys); break;
     }
-    fun(ts, ys, r, aux);
+    if constexpr (IsTeam<P>::value) fun.stage(s, ts, ys, r);   // the block's four waves together
+    else fun(ts, ys, r, aux);
     if (s < 6) K.put_stage(s, r);
   }
   // after the loop: ys = y + h*(B . K[:6]) = y_new, r = K6
@@ -1453,6 +1500,7 @@ __device__ __forceinline__ double dp54_attempt(const P& fun, KS& K, double t, co
     const double x = e / sc;
     ss = (v == 0) ? x * x : ss + x * x;
   }
+  RWRT_STAMP(6);
   if (Kout) {
 #pragma unroll
     for (int j = 0; j < 6; ++j)
@@ -1531,7 +1579,7 @@ struct Lane {
         return kFrozen;
       }
       if (t == tb) return kReached;
-      if (!P::kAutonomous) fun(t, y, f);   // rkf45.py:378 (equal to K6 if autonomous)
+      if constexpr (!P::kAutonomous) fun(t, y, f);   // rkf45.py:378 (equal to K6 if autonomous)
       hs = np_max(habs, min_step);         // rkf45.py:383-387
       rejected = false;
       in_step = true;
@@ -1572,6 +1620,7 @@ struct Lane {
     rejected = rejected || !acc;
     nacc += acc ? 1 : 0;
     nrej += acc ? 0 : 1;
+    RWRT_STAMP(7);
     return (acc && t - tb >= 0.0) ? kReached : kStep;   // rkf45.py:250
   }
 };
@@ -1697,9 +1746,9 @@ struct RunArgs {
   int64_t* count;
   int32_t* nanrow;
   double* out;
-  int32_t* queue;       // [0] heavy-queue head, [1] light-queue head
-  int64_t n_heavy;      // order[0, n_heavy) = heavy queue, the rest = light queue
-  int32_t heavy_blocks; // blocks [0, heavy_blocks) serve the heavy queue first
+  int32_t* queue;       // [1]: the work queue's head ([0] unused)
+  int64_t n_heavy;      // order[0, n_heavy): rays of rk45_team_kernel (latency mode); the queue is the rest
+  int32_t heavy_blocks; // (unused)
   double cut_a;         // haversine argument certainly below cut_off (cal_dis_below)
   const uint8_t* frozen;  // rays frozen at the launch start (NULL: none skipped), see frozen_fill_kernel
 };
@@ -1720,10 +1769,9 @@ inline double haversine_cut(double cut_off) {
 //
 // Load balance: the work per ray per chunk spans 15x the mean (C3); the
 // slowest rays set the makespan.  The host orders rays by the work they did in
-// the previous chunk and hands the heaviest ones to one high-priority wave per
-// SIMD (blocks [0, heavy_blocks), s_setprio 3): those rays' lanes get the
-// SIMD's issue slots first and the critical path runs at single-wave speed,
-// while the normal-priority waves fill every stall.
+// the previous chunk (longest first) and may hand the heaviest ones to
+// rk45_team_kernel (latency mode, order[0, n_heavy)); this kernel's queue is
+// the rest.
 #ifndef RWRT_WAVES_PER_SIMD
 #define RWRT_WAVES_PER_SIMD 1
 #endif
@@ -1751,6 +1799,9 @@ __global__ void __launch_bounds__(256, RWRT_WAVES_PER_SIMD) rk45_run_kernel(RunA
   __shared__ __attribute__((aligned(16))) char smem[kKBytes + LaneBG<BG>::kLdsBytes];
   const RayProblem P{LaneBG<BG>::make(a.B, smem + kKBytes)};
   const int64_t nrows = a.it_end - a.it_begin;
+#if RWRT_DIAG_STAMPS
+  s_stamp_last[(threadIdx.x >> 6) & 3] = __builtin_amdgcn_s_memtime();
+#endif
 #if RWRT_K_IN_LDS
   Lane<RayProblem, KStore> L;
   L.K.p = reinterpret_cast<double*>(smem) + threadIdx.x;
@@ -1761,29 +1812,15 @@ __global__ void __launch_bounds__(256, RWRT_WAVES_PER_SIMD) rk45_run_kernel(RunA
   int64_t ray = -1, nacc = 0, nrej = 0;
   int32_t it = 0, nanrow = 0;
   double prev_lon = 0.0, prev_lat = 0.0, cos_prev = 0.0;
-  const bool heavy = (int)blockIdx.x < a.heavy_blocks;
-  bool heavy_left = heavy && a.n_heavy > 0;
-  if (heavy) {
-    __builtin_amdgcn_s_setprio(3);
-  } else if (RWRT_RUN_PRIO) {
+  if (RWRT_RUN_PRIO) {
     // above frozen_fill_kernel's waves (priority 0) sharing the SIMD: the
     // fill takes the issue cycles the ray loop leaves idle
     __builtin_amdgcn_s_setprio(1);
   }
   for (;;) {
     if (ray < 0) {
-      int64_t w = -1;
-      if (heavy_left) {
-        w = atomicAdd(&a.queue[0], 1);
-        if (w >= a.n_heavy) {
-          heavy_left = false;
-          w = -1;
-        }
-      }
-      if (w < 0) {
-        w = a.n_heavy + atomicAdd(&a.queue[1], 1);
-        if (w >= a.nray) break;
-      }
+      const int64_t w = a.n_heavy + atomicAdd(&a.queue[1], 1);
+      if (w >= a.nray) break;
       ray = a.order ? a.order[w] : w;
       if (a.frozen && a.frozen[ray]) {   // its rows come from frozen_fill_kernel
         ray = -1;
@@ -1811,6 +1848,7 @@ __global__ void __launch_bounds__(256, RWRT_WAVES_PER_SIMD) rk45_run_kernel(RunA
     const double tb = a.tbound[it];
     const int st = L.iterate(P, tb, a.min_step, a.rtol, a.atol, nacc, nrej);
     if (st == Lane<RayProblem, KStore>::kStep) continue;
+    RWRT_STAMP(8);
 
     // ---- interval it reached: post-processing (wr.py:835-885) ----
     // The last accepted step's K6 evaluation was at this y: its cos(lat), ug
@@ -1867,6 +1905,7 @@ __global__ void __launch_bounds__(256, RWRT_WAVES_PER_SIMD) rk45_run_kernel(RunA
       }
     }
     if (nanrow == a.nt && isnan(y[0])) nanrow = it;  // wr.py:853-855 (host reduces)
+    RWRT_STAMP(9);
     prev_lon = y[0];
     prev_lat = y[1];
     cos_prev = cos_c;
@@ -1987,6 +2026,268 @@ frozen_fill_kernel(RunArgs<BG> a) {
     // lookups wait in
     for (int64_t z = RWRT_FILL_THROTTLE; z <= nrows; z += RWRT_FILL_THROTTLE) __builtin_amdgcn_s_sleep(RWRT_FILL_SLEEP);
 #endif
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Latency mode: rk45_team_kernel.  One ray per lane as in rk45_run_kernel, but
+// each RHS evaluation of a ray is split over the four waves of its block --
+// one per SIMD -- so that the independent pieces of wr.py:492-556 run side by
+// side instead of one after another on one SIMD:
+//
+//   phase 1  wave 0: the bilinear lookup (cell cache)  wave 1: sin, cos of lat
+//            wave 2: tan of lat                        (bs.py:781-887)
+//   phase 2  wave 0: fu/cos, fv/cos   wave 1: ux/cos, vx/cos   (bs.py:862-883)
+//            wave 2: cal_ugvg's two quotients (wn.py:266-294)
+//            wave 3: core_diffun's qk, ql and damp2 (wr.py:53-78)
+//   phase 3  wave 0: damp1 -> damp -> dy4   wave 1: dy0, dy1   wave 2: dy2, dy3
+//
+// exchanging values through LDS between the phases (three barriers per RHS).
+// Everything else -- stage inputs, step control, pow, the interval masks -- is
+// computed by all four waves on identical values, so their control flow (and
+// with it every barrier) stays the same; wave 0 alone writes to memory.  Each
+// value is the same operation on the same operands as in ray_rhs, so the
+// results are the run kernel's bit for bit (tests/test_gpu_team.py).  A ray's
+// attempt then costs roughly the longest phase chain instead of the whole
+// instruction stream: the tail of a launch (the heaviest rays, C3/C4) runs
+// ~2-3x faster, at a quarter of the rays per SIMD.
+// ---------------------------------------------------------------------------
+enum TeamSlot {
+  TX_G = 0,                          // g[11] (phase 1, wave 0)
+  TX_S = 11, TX_C, TX_TN,            // sin, cos, tan of lat (waves 1, 2)
+  TX_DU, TX_DV, TX_DUX, TX_DVX,      // the four Mercator quotients (waves 0, 1)
+  TX_QU, TX_QV,                      // cal_ugvg's quotients (wave 2)
+  TX_QK, TX_QL, TX_DAMP2,            // core_diffun's (wave 3)
+  kTeamSlots
+};
+constexpr int kTeamLanes = 64;
+
+// K1..K6 of the block's rays in LDS, [stage][variable][lane]: written by the
+// RHS's phase 3, read by every wave (K0 is the step's f, in registers)
+struct KTeam {
+  double* p;   // this lane's column
+  __device__ __forceinline__ double get(int j, int v) const { return p[(j * 5 + v) * kTeamLanes]; }
+  __device__ __forceinline__ void put_stage(int, const double*) {}
+};
+
+__device__ __forceinline__ void k_sincos(double x, double& s, double& c) {
+#if RWRT_MATH_NUMPY
+  np_math::nm_sincos(x, s, c);      // == nm_sincostan's s, c
+#else
+  double t;
+  k_sincostan(x, s, c, t);
+#endif
+}
+
+struct TeamRHS {
+  static constexpr int NV = 5;
+  static constexpr int NAUX = 0;
+  static constexpr bool kAutonomous = true;
+  static constexpr bool kTeam = true;
+  CachedStaticBG B;   // wave 0's lookup cache
+  double* X;          // [kTeamSlots][64]
+  double* K;          // [7][5][64]
+  unsigned lane;
+  int role;           // wave index in the block (uniform)
+  __device__ __forceinline__ double& x(int s) const { return X[s * kTeamLanes + lane]; }
+  __device__ __forceinline__ double& k(int j, int v) const { return K[(j * 5 + v) * kTeamLanes + lane]; }
+
+  // ray_rhs for stage s (1..6) of the lane's ray, the block's four waves
+  // together; dy = K_s
+  __device__ __forceinline__ void stage(int s, double t, const double* y, double* dy) const {
+    const double lon = y[0], lat = y[1], kx = y[2];
+    const bool bad = fabs(lat) >= kHalfPi || fabs(y[3]) >= 100.0;
+    const double ky = bad ? kNaN : y[3], amp = y[4];
+    // ---- phase 1: lookup | sin, cos | tan
+    if (role == 0) {
+      double g[11];
+      const auto pending = lookup_begin(B, lon, lat, t);
+      lookup_end(B, pending, g);
+#pragma unroll
+      for (int q = 0; q < 11; ++q) x(TX_G + q) = g[q];
+    } else if (role == 1) {
+      double sn, cs;
+      k_sincos(lat, sn, cs);
+      x(TX_S) = sn;
+      x(TX_C) = cs;
+    } else if (role == 2) {
+      x(TX_TN) = k_tan(lat);
+    }
+    __syncthreads();
+    const double sn = x(TX_S), c = x(TX_C), tn = x(TX_TN);
+    const Merc M = merc_factors(lat, c, sn);
+    const double cp = M.cp, m = M.m;   // cp == c off the pole band (c * 1.0 + 0.0 * 1e-6)
+    const bool mk = m != 1.0;          // mercator12_masked's extra factor
+    const double fu = x(TX_G + F_U), fv = x(TX_G + F_V);
+    const double fqx = x(TX_G + F_QX), fqy = x(TX_G + F_QY);
+    const double fqxx = x(TX_G + F_QXX), fqxy = x(TX_G + F_QXY), fqyy = x(TX_G + F_QYY);
+    // the Mercator outputs without a division (bs.py:862-883)
+    const double o6 = mk ? fqx * m : fqx;
+    const double o7 = mk ? (fqy * cp) * m : fqy * cp;
+    const double o8 = mk ? fqxx * m : fqxx;
+    const double o10 = mk ? (fqxy * cp) * m : fqxy * cp;
+    const double o9 = mk ? o10 * m : o10;
+    const double o11 = mk ? (((fqyy * cp) - (fqy * M.s)) * cp) * m : ((fqyy * cp) - (fqy * M.s)) * cp;
+    // ---- phase 2: the quotients
+    if (role == 0) {
+      double du, dv;
+      div2(fu, cp, fv, cp, du, dv);
+      x(TX_DU) = du;
+      x(TX_DV) = dv;
+    } else if (role == 1) {
+      double dux, dvx;
+      div2(x(TX_G + F_UX), cp, x(TX_G + F_VX), cp, dux, dvx);
+      x(TX_DUX) = dux;
+      x(TX_DVX) = dvx;
+    } else if (role == 2) {
+      // cal_ugvg(mode='extent') with l = ky (ugvg())
+      const double kap = RDIV(ky, kx);
+      const double kap2 = kap * kap;
+      const double kap1 = 1.0 + kap2;
+      const double KK = (kx * kx) * kap1;
+      const double denom = KK * kap1;
+      double qu, qv;
+      div2(((1.0 - kap2) * o7) - ((2.0 * kap) * o6), denom,
+           ((2.0 * kap) * o7) + ((1.0 - kap2) * o6), denom, qu, qv);
+      x(TX_QU) = qu;
+      x(TX_QV) = qv;
+    } else {
+      // core_diffun's quotients that need no Mercator quotient
+      const double kap = RDIV(ky, kx);
+      const double kap2 = kap * kap;
+      const double kap1 = 1.0 + kap * kap;
+      const double kk = (kx * kx) * kap1;
+      double qk, ql;
+      div2(kap * o8 - o10, kk, kap * o9 - o11, kk, qk, ql);
+      x(TX_QK) = qk;
+      x(TX_QL) = ql;
+      x(TX_DAMP2) = (2.0 * (kap * (o8 - o11) + (kap2 - 1.0) * o9)) / (kk * kap1);
+    }
+    __syncthreads();
+    // ---- phase 3: the derivatives
+    if (role < 3) {
+      const double fmu = mk ? x(TX_DU) * m : x(TX_DU);
+      const double fmv = mk ? x(TX_DV) * m : x(TX_DV);
+      if (role == 1) {
+        double d0, d1;
+        div2(fmu + x(TX_QU), kREarth, (fmv + x(TX_QV)) * c, kREarth, d0, d1);
+        k(s, 0) = d0;
+        k(s, 1) = d1;
+      } else {
+        const double fmux = mk ? x(TX_DUX) * m : x(TX_DUX);
+        const double fmvx = mk ? x(TX_DVX) * m : x(TX_DVX);
+        const double fmuy = mk ? (x(TX_G + F_UY) + tn * fu) * m : x(TX_G + F_UY) + tn * fu;
+        const double fmvy = mk ? (x(TX_G + F_VY) + tn * fv) * m : x(TX_G + F_VY) + tn * fv;
+        const double kap = RDIV(ky, kx);
+        if (role == 0) {
+          const double kap1 = 1.0 + kap * kap;
+          const double damp1 = (2.0 * ((fmux + fmvy) + kap * (fmvx + fmuy))) / kap1;
+          const double damp3 = (-2.0 * sn) * fmv;
+          const double damp = (damp1 + x(TX_DAMP2)) + damp3;
+          k(s, 4) = div_rearth(damp * amp);
+        } else {
+          double d2, d3;
+          div2((-kx) * ((fmux + kap * fmvx) + x(TX_QK)), kREarth,
+               (-kx) * ((fmuy + kap * fmvy) + x(TX_QL)), kREarth, d2, d3);
+          k(s, 2) = d2;
+          k(s, 3) = d3;
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int v = 0; v < 5; ++v) dy[v] = k(s, v);
+  }
+};
+
+// rows [it_begin, it_end) of rays order[0, n_heavy): one ray per lane (64 per
+// block, no queue), rk45_run_kernel's loop and post-processing otherwise
+__global__ void __launch_bounds__(256, 1) rk45_team_kernel(RunArgs<StaticBG> a) {
+  nm_stage<NM_ALL>();
+  __shared__ __attribute__((aligned(16))) char cache[kCacheBytesPerWave];
+  __shared__ double X[kTeamSlots * kTeamLanes];
+  __shared__ double Kb[7 * 5 * kTeamLanes];
+  const unsigned lane = threadIdx.x & 63u;
+  const int role = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const TeamRHS P{CachedStaticBG{a.B.F, cache, lane * 16u, ~0u, ~0u}, X, Kb, lane, role};
+  const int64_t nrows = a.it_end - a.it_begin;
+  const int64_t w = blockIdx.x * (int64_t)kTeamLanes + lane;
+  int64_t ray = (w < a.n_heavy) ? a.order[w] : -1;
+  Lane<TeamRHS, KTeam> L;
+  L.K.p = Kb + lane;
+  int64_t nacc = 0, nrej = 0;
+  int32_t it = a.it_begin, nanrow = 0;
+  double prev_lon = 0.0, prev_lat = 0.0, cos_prev = 0.0;
+  if (ray >= 0) {
+#pragma unroll
+    for (int v = 0; v < 5; ++v) {
+      L.y[v] = a.state[v * a.nray + ray];
+      L.f[v] = a.state[(5 + v) * a.nray + ray];
+    }
+    L.t = a.state[10 * a.nray + ray];
+    L.habs = a.state[11 * a.nray + ray];
+    L.in_step = false;
+    L.rejected = false;
+    L.hs = 0.0;
+    nacc = a.count[2 * ray];
+    nrej = a.count[2 * ray + 1];
+    nanrow = a.nanrow[ray];
+    prev_lon = L.y[0];
+    prev_lat = L.y[1];
+    cos_prev = k_cos(prev_lat);
+  }
+  while (ray >= 0) {
+    const double tb = a.tbound[it];
+    const int st = L.iterate(P, tb, a.min_step, a.rtol, a.atol, nacc, nrej);
+    if (st == Lane<TeamRHS, KTeam>::kStep) continue;
+    // interval it reached: rk45_run_kernel's post-processing (wr.py:835-885)
+    // with cos(lat), ug and vg recomputed at y (the values its K6 reuse gives)
+    double* y = L.y;
+    double ug = kNaN, vg = kNaN, cos_c = kNaN;
+    bool masked = fabs(y[1]) >= kHalfPi;
+    if (!masked) {
+      cos_c = cos_small(y[1]);
+      masked = cal_dis_reaches(y[0], y[1], prev_lon, prev_lat, cos_c, cos_prev, a.cut_off, a.cut_a);
+    }
+    if (masked) {
+#pragma unroll
+      for (int v = 0; v < 5; ++v) y[v] = kNaN;
+      cos_c = kNaN;
+    }
+    const int last = (st == Lane<TeamRHS, KTeam>::kFrozen) ? a.it_end : it + 1;
+    if (role == 0) {
+      if (!masked) ugvg_at(a.B, tb, y[0], y[1], y[2], y[3], ug, vg);
+      const double2 r0 = make_double2(y[0], y[1]), r1 = make_double2(y[2], y[3]);
+      const double2 r2 = make_double2(y[4], ug), r3 = make_double2(vg, (double)nacc);
+      for (int kr = it; kr < last; ++kr) {
+        double2* o = reinterpret_cast<double2*>(a.out + ((size_t)ray * nrows + (kr - a.it_begin)) * RWRT_NOUT);
+        o[0] = r0;
+        o[1] = r1;
+        o[2] = r2;
+        o[3] = r3;
+      }
+    }
+    if (nanrow == a.nt && isnan(y[0])) nanrow = it;   // wr.py:853-855 (host reduces)
+    prev_lon = y[0];
+    prev_lat = y[1];
+    cos_prev = cos_c;
+    it = last;
+    if (st == Lane<TeamRHS, KTeam>::kFrozen) L.t = a.tbound[a.it_end - 1];
+    if (it == a.it_end) {
+      if (role == 0) {
+#pragma unroll
+        for (int v = 0; v < 5; ++v) {
+          a.state[v * a.nray + ray] = y[v];
+          a.state[(5 + v) * a.nray + ray] = L.f[v];
+        }
+        a.state[10 * a.nray + ray] = L.t;
+        a.state[11 * a.nray + ray] = L.habs;
+        a.count[2 * ray] = nacc;
+        a.count[2 * ray + 1] = nrej;
+        a.nanrow[ray] = nanrow;
+      }
+      ray = -1;
+    }
   }
 }
 
@@ -2454,7 +2755,8 @@ struct rwrt_ctx {
   uint8_t* flags = nullptr;
   size_t cap = 0;
   hipStream_t side = nullptr;
-  hipEvent_t flagged = nullptr, filled = nullptr;
+  hipStream_t team = nullptr;   // rk45_team_kernel (latency mode)
+  hipEvent_t flagged = nullptr, filled = nullptr, team_go = nullptr, team_end = nullptr;
   hipEvent_t done = nullptr;   // end of the last call on this context
   bool used = false;
   std::mutex mu;
@@ -2548,6 +2850,12 @@ rwrt_status launch_run(rwrt_ctx* ctx, const BG& B, int64_t nray, const rwrt_para
     return fail(RWRT_ERR_ARG, "output rows must be 16-byte aligned%s");
   if (nray == 0) return RWRT_OK;
   if (n_heavy < 0 || n_heavy > nray) return fail(RWRT_ERR_ARG, "n_heavy out of range%s");
+  if (n_heavy > 0 && !d_order) return fail(RWRT_ERR_ARG, "n_heavy > 0 needs d_order%s");
+  if (n_heavy > 0 && !std::is_same<BG, StaticBG>::value)
+    return fail(RWRT_ERR_ARG, "latency mode (n_heavy > 0) runs on the static background only%s");
+  const int64_t team_blocks = (n_heavy + kTeamLanes - 1) / kTeamLanes;
+  if (team_blocks > ctx->ncu / 2)
+    return fail(RWRT_ERR_ARG, "n_heavy exceeds the latency mode's capacity (64 rays per CU, half the CUs)%s");
   std::lock_guard<std::mutex> lock(ctx->mu);
   DeviceGuard dg(ctx->device);
   if (!dg.ok) return check_launch("hipSetDevice(context device)");
@@ -2555,14 +2863,14 @@ rwrt_status launch_run(rwrt_ctx* ctx, const BG& B, int64_t nray, const rwrt_para
   if (hipMemsetAsync(d_work, 0, 2 * sizeof(int32_t), st) != hipSuccess)
     return check_launch("hipMemsetAsync(queue)");
   int64_t blocks = ctx_persistent_blocks<BG>(ctx);
-  const int64_t need = (nray + 255) / 256;
+  // latency-mode blocks take a CU each (their LDS does not fit beside a
+  // persistent block): the persistent grid shrinks by as many CUs
+  if (team_blocks) blocks = std::max<int64_t>(1, blocks - team_blocks * (blocks / ctx->ncu));
+  const int64_t need = (nray - n_heavy + 255) / 256;
   if (blocks > need) blocks = need;
-  // one high-priority block per CU when at least two blocks share each CU
-  const int ncu = ctx->ncu;
-  const int heavy_blocks = (d_order && n_heavy > 0 && blocks >= 2 * (int64_t)ncu) ? ncu : 0;
   RunArgs<BG> a{B, nray, p->rtol, p->atol, p->min_step, p->cut_off, p->nt, it_begin, it_end,
                 d_tbound, d_order, d_state, d_count, d_nanrow, d_out, d_work,
-                heavy_blocks ? n_heavy : 0, heavy_blocks, haversine_cut(p->cut_off), nullptr};
+                n_heavy, 0, haversine_cut(p->cut_off), nullptr};
 #if RWRT_FROZEN_FILL
   // frozen rays: flagged on `stream`, filled on the context's side stream
   // while the run kernel (which skips them) integrates the rest; `stream` then
@@ -2575,8 +2883,24 @@ rwrt_status launch_run(rwrt_ctx* ctx, const BG& B, int64_t nray, const rwrt_para
       }))
     return s;
 #endif
-  hipLaunchKernelGGL(rk45_run_kernel<BG>, dim3((unsigned)blocks), dim3(256), 0, st, a);
-  if (rwrt_status s = check_launch("rk45_run_kernel")) return s;
+  if (team_blocks) {
+    // latency mode on the context's team stream, after the flags (and
+    // everything before this call on `stream`); `stream` waits for it below
+    if (hipEventRecord(ctx->team_go, st) != hipSuccess || hipStreamWaitEvent(ctx->team, ctx->team_go, 0) != hipSuccess)
+      return check_launch("hipEventRecord(latency mode start)");
+    if constexpr (std::is_same<BG, StaticBG>::value) {
+      hipLaunchKernelGGL(rk45_team_kernel, dim3((unsigned)team_blocks), dim3(256), 0, ctx->team, a);
+      if (rwrt_status s = check_launch("rk45_team_kernel")) return s;
+    }
+    if (hipEventRecord(ctx->team_end, ctx->team) != hipSuccess)
+      return check_launch("hipEventRecord(latency mode end)");
+  }
+  if (nray > n_heavy) {
+    hipLaunchKernelGGL(rk45_run_kernel<BG>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+    if (rwrt_status s = check_launch("rk45_run_kernel")) return s;
+  }
+  if (team_blocks && hipStreamWaitEvent(st, ctx->team_end, 0) != hipSuccess)
+    return check_launch("hipStreamWaitEvent(latency mode end)");
 #if RWRT_FROZEN_FILL
   hipLaunchKernelGGL(frozen_fill_kernel<BG>, dim3((unsigned)((nray + kFillThreads - 1) / kFillThreads)),
                      dim3(kFillThreads), 0, ctx->side, a);
@@ -2752,6 +3076,9 @@ rwrt_status rwrt_ctx_create(int32_t device, rwrt_ctx** out) {
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
     c->ncu = ncu;
   if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->team, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->team_go, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->team_end, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->flagged, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->filled, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->done, hipEventDisableTiming) != hipSuccess) {
@@ -2773,6 +3100,9 @@ rwrt_status rwrt_ctx_destroy(rwrt_ctx* c) {
     if (c->used && hipEventSynchronize(c->done) != hipSuccess) s = check_launch("rwrt_ctx_destroy");
     if (c->flags) (void)hipFree(c->flags);
     if (c->side) (void)hipStreamDestroy(c->side);
+    if (c->team) (void)hipStreamDestroy(c->team);
+    if (c->team_go) (void)hipEventDestroy(c->team_go);
+    if (c->team_end) (void)hipEventDestroy(c->team_end);
     if (c->flagged) (void)hipEventDestroy(c->flagged);
     if (c->filled) (void)hipEventDestroy(c->filled);
     if (c->done) (void)hipEventDestroy(c->done);
@@ -3013,6 +3343,18 @@ rwrt_status rwrt_selftest_math(int32_t kind, int64_t n, const double* d_x, const
                      n, d_x, d_y, d_out);
   return check_launch("math_kernel");
 }
+
+#if RWRT_DIAG_STAMPS
+// (diagnostic build only; not part of include/rwrt.h) the section cycle sums
+// since the previous call, then zeroed
+rwrt_status rwrt_diag_stamps(unsigned long long* out16) {
+  if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_stamp), sizeof(unsigned long long) * 16) != hipSuccess)
+    return check_launch("rwrt_diag_stamps");
+  unsigned long long z[16] = {};
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamp), z, sizeof(z)) != hipSuccess) return check_launch("rwrt_diag_stamps");
+  return RWRT_OK;
+}
+#endif
 
 // Host side of the drop-in delivery (hostio.HistorySink): the block starts as
 // copies of the previous row, then the shipped columns are scattered in.

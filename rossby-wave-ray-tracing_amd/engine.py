@@ -269,9 +269,32 @@ class RayEngine:
         key = torch.where(frozen, torch.full_like(work, -1), work)
         return torch.sort(key, descending=True, stable=True).indices.to(torch.int64).contiguous()
 
-    def heavy_lanes(self):
-        """Lanes of the high-priority waves (one 256-thread block per CU)."""
-        return torch.cuda.get_device_properties(self.device).multi_processor_count * 256
+    def team_capacity(self):
+        """Rays the latency mode takes at most (64 per CU, half the CUs)."""
+        return (torch.cuda.get_device_properties(self.device).multi_processor_count // 2) * 64
+
+    def team_size(self, team, st, work, order, rows):
+        """How many of the first rays of ``order`` (live at the launch start)
+        go to the latency mode.  An int asks for that many; "auto" takes the
+        rays whose previous-launch work exceeds the launch's fair share per
+        lane (the total over the persistent lanes), which would otherwise
+        outlast the rest."""
+        if order is None or self.bg is not None:   # (the latency mode is static-background only)
+            return 0
+        live = ~torch.isnan(st["state"][:5].sum(0))
+        n_live = int(live.sum().item())
+        cap = min(self.team_capacity(), n_live)
+        if team != "auto":
+            n = min(int(team), cap)
+            # the first n entries of the order must be live rays
+            return n if n == 0 or bool(live[order[:n]].all()) else 0
+        if work is None:
+            return 0
+        w = torch.where(live, work, torch.zeros_like(work))
+        lanes = torch.cuda.get_device_properties(self.device).multi_processor_count * 256
+        share = float(w.sum().item()) / lanes
+        n = int((w > 1.5 * share).sum().item())
+        return min(n, cap)
 
     def run(self, st, p, tbound, it_begin, it_end, out, order=None, n_heavy=0):
         """Rows ``[it_begin, it_end)`` into ``out[nray, it_end-it_begin, 8]`` (async)."""
@@ -336,13 +359,17 @@ class RayEngine:
 
     def integrate(self, y0, nt, tstep, rtol=1e-6, atol=1e-6, msf=1e-3, cut_off=0.1,
                   ttotal=None, chunk=None, sink=None, out=None, cut_rad=None, events=None,
-                  group=None, order_policy="priority", first_chunk=None):
+                  group=None, order_policy="priority", first_chunk=None, team=0):
         """The whole ray loop for ``y0[5, nray]``; rows 1..nt-1 go to ``sink``.
 
         ``sink(i0, i1, rows)`` receives each time chunk as a device tensor
         ``rows[nray, i1-i0, 8]`` (lon lat k l amp ug vg nacc) before the next
         chunk overwrites it.  ``first_chunk`` (int or list) sets short leading
-        chunks whose measured per-ray work orders the next one.  ``events`` (a list) collects a pair of timing
+        chunks whose measured per-ray work orders the next one.  ``team``: rays
+        integrated in latency mode per launch (rk45_team_kernel: each ray's
+        RHS over the four SIMDs of a CU) -- an int (the heaviest rays by the
+        previous launch's work, or the first live ones before any) or "auto"
+        (``team_size``).  ``events`` (a list) collects a pair of timing
         events around every ray-loop launch.  With a process ``group`` (rays
         sharded over ranks, shard.py) the two global outcomes -- solver
         failure and the all-NaN early exit -- are decided over every rank, so a
@@ -367,11 +394,11 @@ class RayEngine:
             return RunResult(cnt[:, 0], cnt[:, 1], st["nanrow"], True, 1, n_live)
         return self.advance(st, p, tb, 1, chunk=chunk, sink=sink, out=out, events=events,
                             group=group, order_policy=order_policy, first_chunk=first_chunk,
-                            n_live=n_live, n_live_local=n_live_local)
+                            n_live=n_live, n_live_local=n_live_local, team=team)
 
     def advance(self, st, p, tb, start, chunk=None, sink=None, out=None, events=None, group=None,
                 order_policy="priority", first_chunk=None, n_live=None, n_live_local=None,
-                prev_work=None):
+                prev_work=None, team=0):
         """Rows ``[start, nt)`` of the ray loop for an initialised state ``st``
         (``init``, or a shard of one: ``take``), in time chunks; the body of
         ``integrate``.  ``prev_work`` (each ray's attempt count, accepted +
@@ -405,11 +432,11 @@ class RayEngine:
         for k, (i0, i1) in enumerate(bounds):
             flat = bufs[k % len(bufs)].view(-1)
             view = flat[: nray * (i1 - i0) * H.NOUT].view(nray, i1 - i0, H.NOUT)
-            n_heavy = 0
+            work = None
             if order_policy in ("cost", "priority") and prev_work is not None:
-                order = self.cost_order(st, cnt.sum(1) - prev_work)
-                if order_policy == "priority":
-                    n_heavy = min(self.heavy_lanes(), n_live_local)
+                work = cnt.sum(1) - prev_work
+                order = self.cost_order(st, work)
+            n_heavy = self.team_size(team, st, work, order, i1 - i0) if team else 0
             prev_work = cnt.sum(1)
             if events is not None:
                 e0, e1, es = self._event_pair()

@@ -43,12 +43,13 @@ def main():
     ap.add_argument("--days", type=float, default=90)
     ap.add_argument("--worlds", default="1,2,4,8")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--bg", default="zonal", choices=["zonal", "nonzonal"])
     a = ap.parse_args()
-    bs, bg = bench.make_bs("zonal")
+    bs, bg = bench.make_bs(a.bg)
     y0 = torch.as_tensor(bench.c3_initial_state(bs), device="cuda")
     eng = RayEngine.from_bs(bs)
     nt = int(a.days * 12) + 1
-    out = {"days": a.days, "worlds": {}}
+    out = {"days": a.days, "bg": a.bg, "worlds": {}}
     for w in [int(x) for x in a.worlds.split(",")]:
         ranks = []
         for r in range(w):
@@ -68,6 +69,11 @@ def main():
     att = int((r1.nacc + r1.nrej).sum().item())
     out["heaviest_ray"] = {"slot": int(full.idx[j].item()), "attempts": att, "s": dt,
                            "us_per_attempt": 1e6 * dt / max(att, 1)}
+    w = work[work > 0].double()
+    q = torch.tensor([0.5, 0.9, 0.99, 0.999, 0.9999], dtype=torch.float64, device=w.device)
+    out["attempts_per_live_ray"] = {"mean": float(w.mean()), "max": int(w.max()),
+                                    "quantiles": dict(zip(["p50", "p90", "p99", "p999", "p9999"],
+                                                          [float(x) for x in torch.quantile(w, q)]))}
     one1 = out["worlds"].get("1")
     if one1:
         for k, v in out["worlds"].items():

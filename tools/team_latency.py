@@ -1,0 +1,80 @@
+"""Latency mode vs the run kernel on the heaviest C3 rays.
+
+    python tools/team_latency.py [--days 90] [--bg zonal] [--out f.json]
+
+Runs the whole C3 set once to find every ray's work (accepted + rejected
+attempts), then integrates the K heaviest rays alone (K = 1, 64, 1024, 8192),
+once through rk45_run_kernel (one ray per lane) and once in latency mode
+(rk45_team_kernel: each ray's RHS split over the four SIMDs of a CU), one
+launch over all rows each, and checks the two agree bit for bit.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "rossby-wave-ray-tracing_amd")]
+import torch  # noqa: E402
+import bench  # noqa: E402
+from engine import RayEngine  # noqa: E402
+
+
+def timed(eng, y0, nt, team, out):
+    kw = dict(ttotal=(nt - 1) * 7200.0, chunk=nt - 1, out=out, team=team)
+    eng.integrate(y0, nt, 7200.0, **kw)
+    torch.cuda.synchronize()
+    best = None
+    for _ in range(2):
+        t0 = time.perf_counter()
+        r = eng.integrate(y0, nt, 7200.0, **kw)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        best = dt if best is None else min(best, dt)
+    return best, r
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--days", type=float, default=90)
+    ap.add_argument("--bg", default="zonal", choices=["zonal", "nonzonal"])
+    ap.add_argument("--ks", default="1,64,1024,8192")
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    bs, _ = bench.make_bs(a.bg)
+    y0 = torch.as_tensor(bench.c3_initial_state(bs), device="cuda")
+    eng = RayEngine.from_bs(bs)
+    nt = int(a.days * 12) + 1
+    full = eng.integrate(y0, nt, 7200.0, ttotal=(nt - 1) * 7200.0, first_chunk=[6, 24, 96])
+    work = (full.nacc + full.nrej)
+    order = torch.sort(work, descending=True, stable=True).indices
+    res = {"days": a.days, "bg": a.bg, "cases": []}
+    for k in [int(x) for x in a.ks.split(",")]:
+        k = min(k, eng.team_capacity())
+        idx = order[:k]
+        yk = y0[:, idx].contiguous()
+        out = torch.empty((k, nt - 1, 8), dtype=torch.float64, device="cuda")
+        t_run, r_run = timed(eng, yk, nt, 0, out)
+        rows_run = out.clone()
+        t_team, r_team = timed(eng, yk, nt, k, out)
+        a_, b_ = rows_run[:, :, :7].cpu().numpy(), out[:, :, :7].cpu().numpy()
+        same = np.array_equal(np.where(np.isnan(a_), np.nan, a_).view(np.int64),
+                              np.where(np.isnan(b_), np.nan, b_).view(np.int64))
+        att = int(work[idx].max().item())
+        c = {"rays": k, "max_attempts": att, "run_kernel_s": t_run, "team_s": t_team,
+             "speedup": t_run / t_team, "run_us_per_attempt": 1e6 * t_run / att,
+             "team_us_per_attempt": 1e6 * t_team / att, "bitwise_equal": bool(same),
+             "counts_equal": bool(torch.equal(r_run.nacc, r_team.nacc) and torch.equal(r_run.nrej, r_team.nrej))}
+        res["cases"].append(c)
+        print(json.dumps(c), flush=True)
+    js = json.dumps(res)
+    print(js)
+    if a.out:
+        open(a.out, "w").write(js + "\n")
+
+
+if __name__ == "__main__":
+    main()
