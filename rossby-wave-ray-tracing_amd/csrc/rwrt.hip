@@ -310,6 +310,7 @@ struct Corners {
   const double* d;  // F[x1, y0]
   double wa, wb, wc, wd;
   unsigned key_x, key_y;   // x0 | x1 << 16, y0 | y1 << 16 (W, H < 2^16)
+  unsigned oa, ob, oc, od; // element offsets of a, b, c, d from F.P
 };
 
 __device__ __forceinline__ Corners corners(const Field& F, double lon, double lat) {
@@ -325,10 +326,14 @@ __device__ __forceinline__ Corners corners(const Field& F, double lon, double la
   // (W, H < 2^24: 24-bit multiplies)
   const unsigned c0 = __umul24(x0, F.H), c1 = __umul24(x1, F.H);
   Corners k;
-  k.a = F.P + __umul24(c0 + y1, kNF);
-  k.b = F.P + __umul24(c1 + y1, kNF);
-  k.c = F.P + __umul24(c0 + y0, kNF);
-  k.d = F.P + __umul24(c1 + y0, kNF);
+  k.oa = __umul24(c0 + y1, kNF);
+  k.ob = __umul24(c1 + y1, kNF);
+  k.oc = __umul24(c0 + y0, kNF);
+  k.od = __umul24(c1 + y0, kNF);
+  k.a = F.P + k.oa;
+  k.b = F.P + k.ob;
+  k.c = F.P + k.oc;
+  k.d = F.P + k.od;
   k.wa = (1.0 - sx) * sy;
   k.wb = sx * sy;
   k.wc = (1.0 - sx) * (1.0 - sy);
@@ -439,13 +444,31 @@ __device__ __forceinline__ void lookup_end(const BG& B, const PendingPoint& p, d
 // the fill's latency overlaps the trigonometry; end() waits for it.  Same
 // values, same blend: results are unchanged.
 //
-// Slice layout (LDS-DMA writes wave base + lane * 16 B): per wave, chunk
-// (corner j, record q) of all 64 lanes at wave_base + (j * 6 + q) * 1 KiB.
+// Slice layout of the time-varying caches (LDS-DMA writes wave base + lane *
+// 16 B): per wave, chunk (corner j, record q) of all 64 lanes at wave_base +
+// (j * 6 + q) * 1 KiB -- a refill is 24 LDS-DMA instructions for the wave.
+// The static cache (RWRT_CACHE_LANE_SLICE) keeps each lane's 24 chunks
+// contiguous instead, at wave_base + lane * 400 B (384 B + 16 B of padding:
+// lanes 16 apart start 64 banks apart, so 16 lanes' ds_read_b128 are
+// conflict-free): the refill of one lane is ONE LDS-DMA instruction whose 24
+// lanes fetch that lane's 24 chunks (refill_lane_slice), so a wave pays an
+// instruction per lane that missed instead of 24 whenever any lane missed.
+// Measured on C3 (profiles/r2/ab/lane_slice.txt): 3.13e9 against 3.44e9 for
+// the chunk-major layout -- the per-lane refill sequence (readlanes, an exec
+// swap, the select and M0 set-up, ~25 instructions) outweighs the 24 LDS-DMA
+// issues it replaces (~21 cycles each, tools/probes/lat_probe.hip) once a
+// few lanes of a wave miss together (every ray a lane pulls starts with a
+// miss), so it is off by default.
 #ifndef RWRT_CELL_CACHE
 #define RWRT_CELL_CACHE 1
 #endif
+#ifndef RWRT_CACHE_LANE_SLICE
+#define RWRT_CACHE_LANE_SLICE 0
+#endif
 constexpr int kCacheChunks = 4 * 6;                        // 4 corners x 6 x 16 B
 constexpr int kCacheBytesPerWave = kCacheChunks * 64 * 16;  // 24 KiB
+constexpr int kSliceStride = 400;                          // bytes per lane (lane-slice layout)
+constexpr int kStaticCacheBytesPerWave = RWRT_CACHE_LANE_SLICE ? 64 * kSliceStride : kCacheBytesPerWave;
 typedef __attribute__((address_space(3))) void* lds_void_ptr;
 typedef __attribute__((address_space(1))) const void* global_void_ptr;
 
@@ -499,21 +522,93 @@ __shared__ unsigned long long s_stamp_last[4];   // per wave of the block
   } while (0)
 #endif
 
+#if RWRT_CACHE_LANE_SLICE
+// Refill lane L's slice (LDS address m0v) with the 24 chunks of its corners
+// (element offsets a, b, c, d from P): ONE global_load_lds_dwordx4 executed
+// by lanes 0..23 whatever the wave's exec mask -- lane i fetches chunk i =
+// (corner i / 6, record i % 6) into m0v + i * 16.  The exec mask is saved
+// and restored around it; the VGPRs written here are asm outputs (dead after
+// it), so no live value of an inactive lane is touched; M0 is restored.
+__device__ __forceinline__ void refill_lane_slice(unsigned m0v, unsigned a, unsigned b, unsigned c,
+                                                  unsigned d, const double* P) {
+  unsigned long long save;
+  unsigned save_m0, vo, vl, vt;
+  asm volatile(
+      "s_mov_b32 %[sm], m0\n\t"
+      "s_mov_b64 %[sv], exec\n\t"
+      "s_mov_b32 exec_lo, 0xffffff\n\t"
+      "s_mov_b32 exec_hi, 0\n\t"
+      "v_mbcnt_lo_u32_b32 %[vl], -1, 0\n\t"
+      "v_mbcnt_hi_u32_b32 %[vl], -1, %[vl]\n\t"
+      "v_mul_u32_u24 %[vt], 43, %[vl]\n\t"
+      "v_lshrrev_b32 %[vt], 8, %[vt]\n\t"          // lane / 6 (lanes < 64)
+      "v_mul_u32_u24 %[vt], 6, %[vt]\n\t"
+      "v_sub_u32 %[vl], %[vl], %[vt]\n\t"
+      "v_lshlrev_b32 %[vl], 4, %[vl]\n\t"          // (lane % 6) * 16 B
+      "v_mov_b32 %[vo], %[d]\n\t"
+      "v_mov_b32 %[vt], %[c]\n\t"
+      "v_cndmask_b32_e64 %[vo], %[vo], %[vt], %[mc]\n\t"
+      "v_mov_b32 %[vt], %[b]\n\t"
+      "v_cndmask_b32_e64 %[vo], %[vo], %[vt], %[mb]\n\t"
+      "v_mov_b32 %[vt], %[a]\n\t"
+      "v_cndmask_b32_e64 %[vo], %[vo], %[vt], %[ma]\n\t"
+      "v_lshl_add_u32 %[vo], %[vo], 3, %[vl]\n\t"    // corner offset * 8 B + chunk
+      "s_mov_b32 m0, %[dst]\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %[vo], %[P]\n\t"
+      "s_mov_b64 exec, %[sv]\n\t"
+      "s_mov_b32 m0, %[sm]"
+      : [sv] "=&s"(save), [sm] "=&s"(save_m0), [vo] "=&v"(vo), [vl] "=&v"(vl), [vt] "=&v"(vt)
+      : [a] "s"(a), [b] "s"(b), [c] "s"(c), [d] "s"(d), [ma] "s"(0x3Full), [mb] "s"(0xFC0ull),
+        [mc] "s"(0x3F000ull), [dst] "s"(m0v), [P] "s"(P)
+      : "memory");
+}
+#endif
+
 struct CachedStaticBG {
   static constexpr bool kTimeVarying = false;
   Field F;
-  char* wave_base;                // this wave's 24 KiB (wave-uniform)
-  unsigned lane16;                // lane * 16
+  char* wave_base;                // this wave's slice area (wave-uniform)
+  unsigned lane16;                // lane * 16 (lane * kSliceStride with RWRT_CACHE_LANE_SLICE)
   mutable unsigned key_x, key_y;  // cell held in the slice (~0u: none)
 
   struct Pending {
     double wa, wb, wc, wd;
   };
   __device__ __forceinline__ const double2& chunk(int j, int q) const {
+#if RWRT_CACHE_LANE_SLICE
+    return *reinterpret_cast<const double2*>(wave_base + lane16 + (j * 6 + q) * 16);
+#else
     return *reinterpret_cast<const double2*>(wave_base + (j * 6 + q) * 1024 + lane16);
+#endif
   }
   __device__ __forceinline__ Pending begin(double lon, double lat) const {
     const Corners k = corners(F, py_mod_2pi(lon), lat);
+#if RWRT_CACHE_LANE_SLICE
+    const bool miss = k.key_x != key_x || k.key_y != key_y;
+    unsigned long long m = __ballot(miss);   // the lanes that changed cell (wave-uniform)
+    if (m) {
+#if RWRT_DIAG_STAMPS
+      RWRT_STAMP(1);
+      if (__lane_id() == __builtin_amdgcn_readfirstlane(__lane_id())) atomicAdd(&g_stamp[11], 1ull);
+#endif
+      typedef __attribute__((address_space(3))) char lds_char;
+      const unsigned base = (unsigned)(size_t)(lds_char*)wave_base;
+      do {
+        const int L = __builtin_ctzll(m);
+        m &= m - 1;
+        refill_lane_slice(base + (unsigned)L * kSliceStride, __builtin_amdgcn_readlane(k.oa, L),
+                          __builtin_amdgcn_readlane(k.ob, L), __builtin_amdgcn_readlane(k.oc, L),
+                          __builtin_amdgcn_readlane(k.od, L), F.P);
+      } while (m);
+      RWRT_STAMP(10);
+    }
+    if (miss) {
+      key_x = k.key_x;
+      key_y = k.key_y;
+    }
+    return Pending{k.wa, k.wb, k.wc, k.wd};
+#else
     if (k.key_x != key_x || k.key_y != key_y) {   // miss: refill the slice by LDS-DMA
 #if RWRT_DIAG_STAMPS
       RWRT_STAMP(1);
@@ -532,6 +627,7 @@ struct CachedStaticBG {
       RWRT_STAMP(10);
     }
     return Pending{k.wa, k.wb, k.wc, k.wd};
+#endif
   }
   __device__ __forceinline__ void end(const Pending& p, double g[11]) const {
     RWRT_STAMP(2);
@@ -856,10 +952,11 @@ struct LaneBG {
 template <>
 struct LaneBG<StaticBG> {
   using type = CachedStaticBG;
-  static constexpr int kLdsBytes = 4 * kCacheBytesPerWave;   // 256-thread blocks
+  static constexpr int kLdsBytes = 4 * kStaticCacheBytesPerWave;   // 256-thread blocks
   __device__ static CachedStaticBG make(const StaticBG& B, char* lds) {
     const unsigned wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    return CachedStaticBG{B.F, lds + wave * kCacheBytesPerWave, (threadIdx.x & 63u) * 16u, ~0u, ~0u};
+    return CachedStaticBG{B.F, lds + wave * kStaticCacheBytesPerWave,
+                          (threadIdx.x & 63u) * (RWRT_CACHE_LANE_SLICE ? kSliceStride : 16u), ~0u, ~0u};
   }
 };
 template <>
@@ -1951,9 +2048,9 @@ __global__ void frozen_flag_kernel(const double* __restrict__ state, int64_t nra
 }
 
 // At most 128 VGPRs: a fill wave must fit beside the run kernel's wave in a
-// SIMD's register file (256 VGPRs + its AGPRs of 512), and its LDS (4.4 KB of
-// row buffers + the 3.5 KB sin/cos table, one wave per block) beside the run
-// kernel's 151 KB, or the fill would wait for the run to end.
+// SIMD's register file (256 VGPRs + its AGPRs of 512), and its LDS (the 3.5
+// KB sin/cos table, one wave per block) beside the run kernel's 155 KB, or
+// the fill would wait for the run to end.
 constexpr int kFillThreads = 64;
 #ifndef RWRT_FILL_THROTTLE
 #define RWRT_FILL_THROTTLE 64
@@ -1961,19 +2058,46 @@ constexpr int kFillThreads = 64;
 #ifndef RWRT_FILL_SLEEP      // s_sleep units (64 clocks) per RWRT_FILL_THROTTLE rows
 #define RWRT_FILL_SLEEP 32
 #endif
+// Every row of a launch for each frozen ray of a fill tile (one wave, ray
+// base + lane): one ray's rows at a time, 16 B per thread, contiguous (a
+// ray's rows are); thread t stores quarter t & 3 of the 64-B row, read from
+// the ray's lane by cross-lane reads -- no LDS, so that a fill wave fits
+// beside rk45_run_kernel's 155 KB block on every CU.
+__device__ __forceinline__ void write_frozen_tile(double* out, int64_t base, int64_t nrows, bool mine,
+                                                  double2 r0, double2 r1, double2 r2, double2 r3) {
+  unsigned long long lanes = __ballot(mine);
+  const int64_t nq = nrows * 4;
+  const int qt = threadIdx.x & 3;
+  while (lanes) {
+    const int j = __builtin_ctzll(lanes);
+    lanes &= lanes - 1;
+    double2* o = reinterpret_cast<double2*>(out + (size_t)(base + j) * nrows * RWRT_NOUT);
+    // (every lane reads lane j's quarters 0..3 in turn and keeps its own)
+    const double2 q0 = make_double2(__shfl(r0.x, j), __shfl(r0.y, j));
+    const double2 q1 = make_double2(__shfl(r1.x, j), __shfl(r1.y, j));
+    const double2 q2 = make_double2(__shfl(r2.x, j), __shfl(r2.y, j));
+    const double2 q3 = make_double2(__shfl(r3.x, j), __shfl(r3.y, j));
+    const double2 v = qt == 0 ? q0 : qt == 1 ? q1 : qt == 2 ? q2 : q3;
+    for (int64_t q = threadIdx.x; q < nq; q += kFillThreads) store_row16<RWRT_NT_FILL>(o + q, v);
+#if RWRT_FILL_THROTTLE
+    // pace the stores (~0.9 us per full 64 rows written; none for shorter
+    // chunks): a full-rate fill floods the memory queues the run kernel's
+    // lookups wait in
+    for (int64_t z = RWRT_FILL_THROTTLE; z <= nrows; z += RWRT_FILL_THROTTLE) __builtin_amdgcn_s_sleep(RWRT_FILL_SLEEP);
+#endif
+  }
+}
+
 template <class BG>
 __global__ void __launch_bounds__(kFillThreads) __attribute__((amdgpu_num_vgpr(128)))
 frozen_fill_kernel(RunArgs<BG> a) {
   nm_stage<NM_SINCOS>();
-  __shared__ double2 rowbuf[kFillThreads][4];
-  __shared__ int list[kFillThreads];
-  __shared__ int cnt;
   const int64_t nrows = a.it_end - a.it_begin;
   const int64_t base = blockIdx.x * (int64_t)kFillThreads;
-  if (threadIdx.x == 0) cnt = 0;
-  __syncthreads();
   const int64_t ray = base + threadIdx.x;
-  if (ray < a.nray && a.frozen[ray]) {
+  const bool mine = ray < a.nray && a.frozen[ray];
+  double2 r0 = make_double2(0.0, 0.0), r1 = r0, r2 = r0, r3 = r0;
+  if (mine) {
     // rk45_run_kernel's fetch + kFrozen iteration + post-processing, verbatim
     double y[5];
 #pragma unroll
@@ -1997,36 +2121,17 @@ frozen_fill_kernel(RunArgs<BG> a) {
     } else {
       ugvg_at(a.B, tb, y[0], y[1], y[2], y[3], ug, vg);
     }
-    const double2 r0 = make_double2(y[0], y[1]), r1 = make_double2(y[2], y[3]);
-    const double2 r2 = make_double2(y[4], ug), r3 = make_double2(vg, (double)nacc);
-    rowbuf[threadIdx.x][0] = r0;
-    rowbuf[threadIdx.x][1] = r1;
-    rowbuf[threadIdx.x][2] = r2;
-    rowbuf[threadIdx.x][3] = r3;
+    r0 = make_double2(y[0], y[1]);
+    r1 = make_double2(y[2], y[3]);
+    r2 = make_double2(y[4], ug);
+    r3 = make_double2(vg, (double)nacc);
     if (nanrow == a.nt && isnan(y[0])) nanrow = it;   // wr.py:853-855
 #pragma unroll
     for (int v = 0; v < 5; ++v) a.state[v * a.nray + ray] = y[v];
     a.state[10 * a.nray + ray] = a.tbound[a.it_end - 1];
     a.nanrow[ray] = nanrow;
-    list[atomicAdd(&cnt, 1)] = threadIdx.x;
   }
-  __syncthreads();
-  // every row of the chunk for each frozen ray of the tile: the block writes
-  // one ray's rows at a time, 16 B per thread, contiguous (a ray's rows are)
-  const int n = cnt;
-  const int64_t nq = nrows * 4;
-  for (int k = 0; k < n; ++k) {
-    const int j = list[k];
-    double2* o = reinterpret_cast<double2*>(a.out + (size_t)(base + j) * nrows * RWRT_NOUT);
-    const double2 v = rowbuf[j][threadIdx.x & 3];
-    for (int64_t q = threadIdx.x; q < nq; q += kFillThreads) store_row16<RWRT_NT_FILL>(o + q, v);
-#if RWRT_FILL_THROTTLE
-    // pace the stores (~0.9 us per full 64 rows written; none for shorter
-    // chunks): a full-rate fill floods the memory queues the run kernel's
-    // lookups wait in
-    for (int64_t z = RWRT_FILL_THROTTLE; z <= nrows; z += RWRT_FILL_THROTTLE) __builtin_amdgcn_s_sleep(RWRT_FILL_SLEEP);
-#endif
-  }
+  write_frozen_tile(a.out, base, nrows, mine, r0, r1, r2, r3);
 }
 
 // ---------------------------------------------------------------------------
@@ -2204,12 +2309,13 @@ struct TeamRHS {
 // block, no queue), rk45_run_kernel's loop and post-processing otherwise
 __global__ void __launch_bounds__(256, 1) rk45_team_kernel(RunArgs<StaticBG> a) {
   nm_stage<NM_ALL>();
-  __shared__ __attribute__((aligned(16))) char cache[kCacheBytesPerWave];
+  __shared__ __attribute__((aligned(16))) char cache[kStaticCacheBytesPerWave];
   __shared__ double X[kTeamSlots * kTeamLanes];
   __shared__ double Kb[7 * 5 * kTeamLanes];
   const unsigned lane = threadIdx.x & 63u;
   const int role = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const TeamRHS P{CachedStaticBG{a.B.F, cache, lane * 16u, ~0u, ~0u}, X, Kb, lane, role};
+  const TeamRHS P{CachedStaticBG{a.B.F, cache, lane * (RWRT_CACHE_LANE_SLICE ? kSliceStride : 16u), ~0u, ~0u},
+                  X, Kb, lane, role};
   const int64_t nrows = a.it_end - a.it_begin;
   const int64_t w = blockIdx.x * (int64_t)kTeamLanes + lane;
   int64_t ray = (w < a.n_heavy) ? a.order[w] : -1;
@@ -2474,15 +2580,12 @@ __global__ void rk4_flag_kernel(const double* __restrict__ state, int64_t nray,
 __global__ void __launch_bounds__(kFillThreads) __attribute__((amdgpu_num_vgpr(128)))
 rk4_fill_kernel(Rk4Args a) {
   nm_stage<NM_SINCOS>();
-  __shared__ double2 rowbuf[kFillThreads][4];
-  __shared__ int list[kFillThreads];
-  __shared__ int cnt;
   const int64_t nrows = a.it_end - a.it_begin;
   const int64_t base = blockIdx.x * (int64_t)kFillThreads;
-  if (threadIdx.x == 0) cnt = 0;
-  __syncthreads();
   const int64_t ray = base + threadIdx.x;
-  if (ray < a.nray && a.frozen[ray]) {
+  const bool mine = ray < a.nray && a.frozen[ray];
+  double2 r0 = make_double2(0.0, 0.0), r1 = r0, r2 = r0, r3 = r0;
+  if (mine) {
     double y[5];
 #pragma unroll
     for (int v = 0; v < 5; ++v) y[v] = a.state[v * a.nray + ray];
@@ -2506,29 +2609,17 @@ rk4_fill_kernel(Rk4Args a) {
     }
     double ug, vg;
     ugvg_at(StaticBG{a.F}, 0.0, y[0], y[1], y[2], y[3], ug, vg);
-    rowbuf[threadIdx.x][0] = make_double2(y[0], y[1]);
-    rowbuf[threadIdx.x][1] = make_double2(y[2], y[3]);
-    rowbuf[threadIdx.x][2] = make_double2(y[4], ug);
-    rowbuf[threadIdx.x][3] = make_double2(vg, (double)nstep);
+    r0 = make_double2(y[0], y[1]);
+    r1 = make_double2(y[2], y[3]);
+    r2 = make_double2(y[4], ug);
+    r3 = make_double2(vg, (double)nstep);
     if (nanrow == a.nt && isnan(y[0])) nanrow = it;
 #pragma unroll
     for (int v = 0; v < 5; ++v) a.state[v * a.nray + ray] = y[v];
     a.count[2 * ray] = nstep;
     a.nanrow[ray] = nanrow;
-    list[atomicAdd(&cnt, 1)] = threadIdx.x;
   }
-  __syncthreads();
-  const int n = cnt;
-  const int64_t nq = nrows * 4;
-  for (int k = 0; k < n; ++k) {
-    const int j = list[k];
-    double2* o = reinterpret_cast<double2*>(a.out + (size_t)(base + j) * nrows * RWRT_NOUT);
-    const double2 v = rowbuf[j][threadIdx.x & 3];
-    for (int64_t q = threadIdx.x; q < nq; q += kFillThreads) store_row16<RWRT_NT_FILL>(o + q, v);
-#if RWRT_FILL_THROTTLE
-    for (int64_t z = RWRT_FILL_THROTTLE; z <= nrows; z += RWRT_FILL_THROTTLE) __builtin_amdgcn_s_sleep(RWRT_FILL_SLEEP);
-#endif
-  }
+  write_frozen_tile(a.out, base, nrows, mine, r0, r1, r2, r3);
 }
 
 // rk45_simple_current (rkf45.py:672-724) over ncol columns, one lane each.
