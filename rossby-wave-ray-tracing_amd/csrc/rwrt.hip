@@ -1059,7 +1059,14 @@ __device__ __forceinline__ double add_rd(double a, double b) {
 }
 }  // namespace rwrt
 #define NM_FN __device__ __forceinline__
+#ifndef RWRT_NM_CONST_MEM
+#define RWRT_NM_CONST_MEM 0
+#endif
+#if RWRT_NM_CONST_MEM   // (experiment) the polynomial constants as scalar loads, not s_mov pairs
+#define NM_CONST __constant__
+#else
 #define NM_CONST constexpr
+#endif
 #define NM_TABLE constexpr
 #define NM_FMA_RZ(a, b, c) ::rwrt::fma_rz((a), (b), (c))
 #define NM_MUL_RZ(a, b) ::rwrt::mul_rz((a), (b))

@@ -359,13 +359,15 @@ class RayEngine:
 
     def integrate(self, y0, nt, tstep, rtol=1e-6, atol=1e-6, msf=1e-3, cut_off=0.1,
                   ttotal=None, chunk=None, sink=None, out=None, cut_rad=None, events=None,
-                  group=None, order_policy="priority", first_chunk=None, team=0):
+                  group=None, order_policy="priority", first_chunk=None, team=0, stop_row=None):
         """The whole ray loop for ``y0[5, nray]``; rows 1..nt-1 go to ``sink``.
 
         ``sink(i0, i1, rows)`` receives each time chunk as a device tensor
         ``rows[nray, i1-i0, 8]`` (lon lat k l amp ug vg nacc) before the next
         chunk overwrites it.  ``first_chunk`` (int or list) sets short leading
-        chunks whose measured per-ray work orders the next one.  ``team``: rays
+        chunks whose measured per-ray work orders the next one.  ``stop_row``
+        ends the run before that row (``RunResult.state`` then holds the
+        solver state for ``checkpoint`` / ``resume``).  ``team``: rays
         integrated in latency mode per launch (rk45_team_kernel: each ray's
         RHS over the four SIMDs of a CU) -- an int (the heaviest rays by the
         previous launch's work, or the first live ones before any) or "auto"
@@ -394,17 +396,18 @@ class RayEngine:
             return RunResult(cnt[:, 0], cnt[:, 1], st["nanrow"], True, 1, n_live)
         return self.advance(st, p, tb, 1, chunk=chunk, sink=sink, out=out, events=events,
                             group=group, order_policy=order_policy, first_chunk=first_chunk,
-                            n_live=n_live, n_live_local=n_live_local, team=team)
+                            n_live=n_live, n_live_local=n_live_local, team=team, stop_row=stop_row)
 
     def advance(self, st, p, tb, start, chunk=None, sink=None, out=None, events=None, group=None,
                 order_policy="priority", first_chunk=None, n_live=None, n_live_local=None,
-                prev_work=None, team=0):
+                prev_work=None, team=0, stop_row=None):
         """Rows ``[start, nt)`` of the ray loop for an initialised state ``st``
         (``init``, or a shard of one: ``take``), in time chunks; the body of
         ``integrate``.  ``prev_work`` (each ray's attempt count, accepted +
         rejected, at the start of an earlier launch) orders the first launch
         longest-first by the attempts since; otherwise live rays go first."""
         nt = int(p.nt)
+        end = nt if stop_row is None else max(int(start), min(int(stop_row), nt))
         nray = st["nray"]
         cnt = st["count"]
         if n_live_local is None:
@@ -418,11 +421,11 @@ class RayEngine:
         lead = [first_chunk] if isinstance(first_chunk, int) else list(first_chunk or [])
         if order_policy in ("cost", "priority"):
             for n in lead:
-                if 0 < n < chunk and i0 < nt:
-                    bounds.append((i0, min(i0 + n, nt)))
+                if 0 < n < chunk and i0 < end:
+                    bounds.append((i0, min(i0 + n, end)))
                     i0 = bounds[-1][1]
-        while i0 < nt:
-            bounds.append((i0, min(i0 + chunk, nt)))
+        while i0 < end:
+            bounds.append((i0, min(i0 + chunk, end)))
             i0 = bounds[-1][1]
         rows_max = max([b - a for a, b in bounds] or [1])
         bufs = _row_buffers(out, nray, rows_max, self.device)
@@ -454,7 +457,52 @@ class RayEngine:
         brk = mx if mx < nt else None
         res = RunResult(cnt[:, 0], cnt[:, 1], st["nanrow"], False, brk, n_live)
         res.bounds = bounds
+        res.state, res.next_row = st, end
         return res
+
+    # ------------------------------------------------------ checkpoint / resume
+    @staticmethod
+    def checkpoint(res):
+        """The solver state after the rows a run produced (the
+        state is 12 fp64 + 3 integers per ray, so resuming = persisting it at an
+        output index): host arrays that ``resume`` continues from bit for bit."""
+        st = res.state
+        return {"state": st["state"].cpu().numpy(), "count": st["count"].cpu().numpy(),
+                "nanrow": st["nanrow"].cpu().numpy(), "next_row": np.int64(res.next_row)}
+
+    @staticmethod
+    def save_checkpoint(ck, path):
+        np.savez(path, **ck)
+
+    @staticmethod
+    def load_checkpoint(path):
+        with np.load(path, allow_pickle=False) as z:
+            ck = {k: z[k] for k in z.files}
+        if set(ck) != {"state", "count", "nanrow", "next_row"} or ck["state"].shape[0] != H.NSTATE:
+            raise ValueError(f"{path}: not an rwrt checkpoint")
+        return ck
+
+    def resume(self, ck, nt, tstep, rtol=1e-6, atol=1e-6, msf=1e-3, cut_off=0.1, ttotal=None,
+               chunk=None, sink=None, out=None, cut_rad=None, events=None, group=None,
+               order_policy="priority", first_chunk=None, team=0, stop_row=None):
+        """Rows ``[ck['next_row'], nt)`` of the run a checkpoint was taken from
+        (the same ``nt``, ``tstep`` and tolerances), into ``sink`` as in
+        ``integrate``: the rows and counters equal an uninterrupted run's."""
+        p = self.params(nt, tstep, rtol, atol, msf, cut_off, cut_rad)
+        tb = torch.as_tensor(t_eval_of(nt, tstep, ttotal), dtype=F64, device=self.device)
+        nray = int(ck["state"].shape[1])
+        st = dict(state=torch.as_tensor(ck["state"], dtype=F64).to(self.device).contiguous(),
+                  count=torch.as_tensor(ck["count"], dtype=torch.int64).to(self.device).contiguous(),
+                  nanrow=torch.as_tensor(ck["nanrow"], dtype=torch.int32).to(self.device).contiguous(),
+                  nray=nray)
+        start = int(ck["next_row"])
+        if not 1 <= start <= nt:
+            raise ValueError(f"checkpoint row {start} outside [1, {nt}]")
+        live = ~torch.isnan(st["state"][:5].sum(0))
+        n_live_local = int(live.sum().item())
+        return self.advance(st, p, tb, start, chunk=chunk, sink=sink, out=out, events=events,
+                            group=group, order_policy=order_policy, first_chunk=first_chunk,
+                            n_live=n_live_local, n_live_local=n_live_local, team=team, stop_row=stop_row)
 
     @staticmethod
     def take(st, idx):
