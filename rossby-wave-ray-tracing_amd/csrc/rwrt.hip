@@ -508,14 +508,26 @@ __device__ __forceinline__ void lds_dma_wait() { asm volatile("s_waitcnt vmcnt(0
 #if RWRT_DIAG_STAMPS
 __device__ unsigned long long g_stamp[16];
 __shared__ unsigned long long s_stamp_last[4];   // per wave of the block
+__shared__ unsigned long long s_stamp_acc[4][16];  // per wave, flushed at the kernel's end
 #define RWRT_STAMP(k)                                                        \
   do {                                                                       \
     const unsigned long long _t = __builtin_amdgcn_s_memtime();             \
     const unsigned _w = (threadIdx.x >> 6) & 3;                              \
     if (__lane_id() == __builtin_amdgcn_readfirstlane(__lane_id()))          \
-      atomicAdd(&g_stamp[k], _t - s_stamp_last[_w]);                         \
+      s_stamp_acc[_w][k] += _t - s_stamp_last[_w];                           \
     s_stamp_last[_w] = _t;                                                   \
   } while (0)
+// (no global atomics inside the loop: they would sit in vmcnt and inflate the
+// LDS-DMA waits being measured)
+__device__ __forceinline__ void stamp_init() {
+  const unsigned w = (threadIdx.x >> 6) & 3;
+  if ((threadIdx.x & 63) < 16) s_stamp_acc[w][threadIdx.x & 63] = 0;
+  s_stamp_last[w] = __builtin_amdgcn_s_memtime();
+}
+__device__ __forceinline__ void stamp_flush() {
+  const unsigned w = (threadIdx.x >> 6) & 3;
+  if ((threadIdx.x & 63) < 16) atomicAdd(&g_stamp[threadIdx.x & 63], s_stamp_acc[w][threadIdx.x & 63]);
+}
 #else
 #define RWRT_STAMP(k) \
   do {                \
@@ -590,7 +602,7 @@ struct CachedStaticBG {
     if (m) {
 #if RWRT_DIAG_STAMPS
       RWRT_STAMP(1);
-      if (__lane_id() == __builtin_amdgcn_readfirstlane(__lane_id())) atomicAdd(&g_stamp[11], 1ull);
+      if (__lane_id() == __builtin_amdgcn_readfirstlane(__lane_id())) s_stamp_acc[(threadIdx.x >> 6) & 3][11] += 1;
 #endif
       typedef __attribute__((address_space(3))) char lds_char;
       const unsigned base = (unsigned)(size_t)(lds_char*)wave_base;
@@ -612,7 +624,7 @@ struct CachedStaticBG {
     if (k.key_x != key_x || k.key_y != key_y) {   // miss: refill the slice by LDS-DMA
 #if RWRT_DIAG_STAMPS
       RWRT_STAMP(1);
-      if (__lane_id() == __builtin_amdgcn_readfirstlane(__lane_id())) atomicAdd(&g_stamp[11], 1ull);
+      if (__lane_id() == __builtin_amdgcn_readfirstlane(__lane_id())) s_stamp_acc[(threadIdx.x >> 6) & 3][11] += 1;
 #endif
       const double* src[4] = {k.a, k.b, k.c, k.d};
       char* const base = lds_slice_base(wave_base);
@@ -1904,7 +1916,7 @@ __global__ void __launch_bounds__(256, RWRT_WAVES_PER_SIMD) rk45_run_kernel(RunA
   const RayProblem P{LaneBG<BG>::make(a.B, smem + kKBytes)};
   const int64_t nrows = a.it_end - a.it_begin;
 #if RWRT_DIAG_STAMPS
-  s_stamp_last[(threadIdx.x >> 6) & 3] = __builtin_amdgcn_s_memtime();
+  stamp_init();
 #endif
 #if RWRT_K_IN_LDS
   Lane<RayProblem, KStore> L;
@@ -2029,6 +2041,9 @@ __global__ void __launch_bounds__(256, RWRT_WAVES_PER_SIMD) rk45_run_kernel(RunA
       ray = -1;
     }
   }
+#if RWRT_DIAG_STAMPS
+  stamp_flush();
+#endif
 }
 
 // ---------------------------------------------------------------------------

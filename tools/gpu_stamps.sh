@@ -18,4 +18,4 @@ print("batch", d["cycles_per_attempt"], d["refills_per_attempt"])
 for k, v in d["sections"].items():
     print("%-45s %6.3f" % (k, v["frac"]))
 PY
-hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -Wno-unused-value -Wno-unused-result -o /tmp/lat_probe tools/probes/lat_probe.hip && timeout -k 5 60 /tmp/lat_probe | tee gpurun_out/lat_probe.txt
+
