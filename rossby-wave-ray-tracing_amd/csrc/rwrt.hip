@@ -465,6 +465,9 @@ __device__ __forceinline__ void lookup_end(const BG& B, const PendingPoint& p, d
 #ifndef RWRT_CACHE_LANE_SLICE
 #define RWRT_CACHE_LANE_SLICE 0
 #endif
+#ifndef RWRT_DMA_WAIT_IF
+#define RWRT_DMA_WAIT_IF 0   // wait for the refill's LDS-DMA only when the wave issued one
+#endif
 constexpr int kCacheChunks = 4 * 6;                        // 4 corners x 6 x 16 B
 constexpr int kCacheBytesPerWave = kCacheChunks * 64 * 16;  // 24 KiB
 constexpr int kSliceStride = 400;                          // bytes per lane (lane-slice layout)
@@ -586,6 +589,7 @@ struct CachedStaticBG {
 
   struct Pending {
     double wa, wb, wc, wd;
+    bool refilled;   // (wave-uniform) some lane of the wave refilled its slice
   };
   __device__ __forceinline__ const double2& chunk(int j, int q) const {
 #if RWRT_CACHE_LANE_SLICE
@@ -619,9 +623,15 @@ struct CachedStaticBG {
       key_x = k.key_x;
       key_y = k.key_y;
     }
-    return Pending{k.wa, k.wb, k.wc, k.wd};
+    return Pending{k.wa, k.wb, k.wc, k.wd, true};
 #else
-    if (k.key_x != key_x || k.key_y != key_y) {   // miss: refill the slice by LDS-DMA
+    const bool miss = k.key_x != key_x || k.key_y != key_y;
+#if RWRT_DMA_WAIT_IF
+    const bool any = __ballot(miss) != 0;
+#else
+    const bool any = true;
+#endif
+    if (miss) {   // miss: refill the slice by LDS-DMA
 #if RWRT_DIAG_STAMPS
       RWRT_STAMP(1);
       if (__lane_id() == __builtin_amdgcn_readfirstlane(__lane_id())) s_stamp_acc[(threadIdx.x >> 6) & 3][11] += 1;
@@ -638,12 +648,14 @@ struct CachedStaticBG {
       key_y = k.key_y;
       RWRT_STAMP(10);
     }
-    return Pending{k.wa, k.wb, k.wc, k.wd};
+    return Pending{k.wa, k.wb, k.wc, k.wd, any};
 #endif
   }
   __device__ __forceinline__ void end(const Pending& p, double g[11]) const {
     RWRT_STAMP(2);
-    lds_dma_wait();
+    // no refill in this evaluation and none pending from an earlier one (each
+    // waited here): the wait would only wait for the wave's row stores
+    if (p.refilled) lds_dma_wait();
     RWRT_STAMP(12);
     Corners k;
     k.wa = p.wa;
@@ -1894,6 +1906,9 @@ inline double haversine_cut(double cut_off) {
 #ifndef RWRT_RUN_PRIO
 #define RWRT_RUN_PRIO 1
 #endif
+#ifndef RWRT_DIAG_NOSTORE
+#define RWRT_DIAG_NOSTORE 0
+#endif
 #ifndef RWRT_DIAG_NOFROZENFILL   // timing-only diagnostic build: frozen rays write one row
 #define RWRT_DIAG_NOFROZENFILL 0
 #endif
@@ -1961,7 +1976,11 @@ __global__ void __launch_bounds__(256, RWRT_WAVES_PER_SIMD) rk45_run_kernel(RunA
       cos_prev = k_cos(prev_lat);
       L.aux[2] = kNaN;     // no evaluation at y yet
     }
+#if RWRT_DIAG_TB_ARITH   // timing-only diagnostic build: t_bound = it * 2 h (the bench's schedule), no load
+    const double tb = (double)it * 7200.0;
+#else
     const double tb = a.tbound[it];
+#endif
     const int st = L.iterate(P, tb, a.min_step, a.rtol, a.atol, nacc, nrej);
     if (st == Lane<RayProblem, KStore>::kStep) continue;
     RWRT_STAMP(8);
@@ -2003,7 +2022,7 @@ __global__ void __launch_bounds__(256, RWRT_WAVES_PER_SIMD) rk45_run_kernel(RunA
     // masks against itself is a no-op), so every remaining row of the chunk
     // equals this one: write them all and release the lane.
     const int last = (st == Lane<RayProblem, KStore>::kFrozen) ? a.it_end : it + 1;
-    {
+    if (!RWRT_DIAG_NOSTORE) {   // (timing-only diagnostic build: no row stores)
       double2* o = reinterpret_cast<double2*>(a.out + ((size_t)ray * nrows + (it - a.it_begin)) * RWRT_NOUT);
       store_row16<RWRT_NT_ROWS>(o + 0, r0);
       store_row16<RWRT_NT_ROWS>(o + 1, r1);
@@ -3015,8 +3034,12 @@ rwrt_status launch_run(rwrt_ctx* ctx, const BG& B, int64_t nray, const rwrt_para
   if (team_blocks && hipStreamWaitEvent(st, ctx->team_end, 0) != hipSuccess)
     return check_launch("hipStreamWaitEvent(latency mode end)");
 #if RWRT_FROZEN_FILL
-  hipLaunchKernelGGL(frozen_fill_kernel<BG>, dim3((unsigned)((nray + kFillThreads - 1) / kFillThreads)),
-                     dim3(kFillThreads), 0, ctx->side, a);
+#ifndef RWRT_DIAG_FILL
+#define RWRT_DIAG_FILL 0   // timing-only diagnostic builds: 1 = no fill launch, 2 = the fill after the run kernel
+#endif
+  if (RWRT_DIAG_FILL != 1)
+    hipLaunchKernelGGL(frozen_fill_kernel<BG>, dim3((unsigned)((nray + kFillThreads - 1) / kFillThreads)),
+                       dim3(kFillThreads), 0, RWRT_DIAG_FILL == 2 ? st : ctx->side, a);
   if (rwrt_status s = check_launch("frozen_fill_kernel")) return s;
   return ctx_end(ctx, st);
 #else
