@@ -66,6 +66,13 @@ void nm_sincos_arr(const double* x, double* s, double* c, int64_t n) {
 void nm_sincostan_arr(const double* x, double* s, double* c, double* t, int64_t n) {
   for (int64_t i = 0; i < n; ++i) nm_sincostan(x[i], s[i], c[i], t[i]);
 }
+// the RHS's split form (nm_sincostan_begin .. nm_sincostan_end)
+void nm_sincostan_split_arr(const double* x, double* s, double* c, double* t, int64_t n) {
+  for (int64_t i = 0; i < n; ++i) {
+    const SinCosTanPre p = nm_sincostan_begin(x[i]);
+    nm_sincostan_end(x[i], p, s[i], c[i], t[i]);
+  }
+}
 void nm_rcp14_arr(const double* x, double* out, int64_t n) {
   for (int64_t i = 0; i < n; ++i) out[i] = nm_rcp14(x[i]);
 }

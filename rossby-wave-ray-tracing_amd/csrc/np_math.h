@@ -335,6 +335,36 @@ NM_FN void nm_sincostan(double x, double& sn, double& cs, double& tn) {
     tn = nm_tan(x);
   }
 }
+// The same in two halves, so that a caller can place independent work
+// (the RHS: the lookup's cell arithmetic) beside the first half's table reads
+// and tan polynomial: nm_sincostan_begin .. nm_sincostan_end(x, ...) gives
+// nm_sincostan's values bit for bit (the same operations on the same operands).
+struct SinCosTanPre {
+  SinCosPre P;
+  TanPre tp;
+  unsigned A, Nk;
+};
+NM_FN SinCosTanPre nm_sincostan_begin(double x) {
+  SinCosTanPre r;
+  const int j = t_index(x);
+  const double T = tabd(kT_TAN_HI, j), Tl = tabd(kT_TAN_LO, j);
+  r.P = nm_sincos_tab(x);
+  NM_ISSUE_FENCE();
+  r.tp = nm_tan_pre(x, T, Tl);
+  const unsigned k = rcp14_knot(r.tp.D);
+  r.A = NM_LD(kRCP14_KNOT, k);
+  r.Nk = NM_LD(kRCP14_KNOT, k + 1);
+  return r;
+}
+NM_FN void nm_sincostan_end(double x, const SinCosTanPre& r, double& sn, double& cs, double& tn) {
+  nm_sincos_fin(x, r.P, sn, cs);
+  tn = nm_tan_fin(r.tp, r.A, r.Nk);
+  if (nm_sincos_rare(x)) {                                    // |x| >= 2.426265, inf, NaN (rare)
+    sn = nm_sin(x);
+    cs = nm_cos(x);
+    tn = nm_tan(x);
+  }
+}
 
 // ---------------------------------------------------------------------------
 // SVML __svml_pow8_ha (main path): log2 x = k + log2 of the table point + a

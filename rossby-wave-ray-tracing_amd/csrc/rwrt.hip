@@ -46,6 +46,9 @@ constexpr double kRInv = 1.0 / 6.3712e6;   // RN(1 / R)
 #ifndef RWRT_RHS_TRIG_SMALL
 #define RWRT_RHS_TRIG_SMALL 1
 #endif
+#ifndef RWRT_TRIG_EARLY
+#define RWRT_TRIG_EARLY 1   // the RHS trigonometry's first half before the lookup's refill branch
+#endif
 #ifndef RWRT_DIV_REARTH_IEEE
 #define RWRT_DIV_REARTH_IEEE 1
 #endif
@@ -1298,15 +1301,23 @@ __device__ __forceinline__ void ray_rhs(const BG& B, double t, const double* y, 
   const double ky = bad ? kNaN : y[3], amp = y[4];
   double g[11];
   RWRT_STAMP(0);
+#if RWRT_TRIG_EARLY && RWRT_MATH_NUMPY && !RWRT_DIAG_NOTRIG
+  // the trigonometry's table reads and tan polynomial beside the lookup's cell
+  // arithmetic (one scheduling region: the refill below is a branch)
+  const auto trig = np_math::nm_sincostan_begin(lat);
+#endif
+  double s, c;
 #if !RWRT_DIAG_NOINTERP
   const auto pending = lookup_begin(B, lon, lat, t);   // the lookup's fill overlaps the trig
 #endif
   RWRT_STAMP(1);
-  double s, c;
 #if RWRT_DIAG_NOTRIG     // timing-only diagnostic build: polynomial stand-ins
   s = lat * (1.0 - lat * lat * (1.0 / 6.0));
   c = 1.0 - lat * lat * 0.5;
   const double tn = lat * (1.0 + lat * lat * (1.0 / 3.0));
+#elif RWRT_TRIG_EARLY && RWRT_MATH_NUMPY
+  double tn;
+  np_math::nm_sincostan_end(lat, trig, s, c, tn);   // == k_sincostan(lat, s, c, tn)
 #else
   double tn;
   k_sincostan(lat, s, c, tn);       // np.cos, np.sin, np.tan of lat (bs.py:856-880)

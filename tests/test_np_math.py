@@ -44,6 +44,7 @@ def lib():
         getattr(lib, n).argtypes = [P, P, I]
     lib.nm_sincos_arr.argtypes = [P, P, P, I]
     lib.nm_sincostan_arr.argtypes = [P, P, P, P, I]
+    lib.nm_sincostan_split_arr.argtypes = [P, P, P, P, I]
     lib.nm_pow_arr.argtypes = [P, P, I, P, I]
     return lib
 
@@ -152,6 +153,19 @@ def test_fused_sincostan_is_sin_cos_tan(lib):
         assert_bitwise(s, np.sin(x), x, "sincostan: sin")
         assert_bitwise(c, np.cos(x), x, "sincostan: cos")
         assert_bitwise(t, np.tan(x), x, "sincostan: tan")
+
+
+def test_split_sincostan_is_sin_cos_tan(lib):
+    """The RHS's split form (nm_sincostan_begin before the lookup's refill
+    branch, nm_sincostan_end after it) == np.sin, np.cos and np.tan."""
+    x = trig_args(np.random.default_rng(6), 1 << 22)
+    x = x[~(np.abs(x) > 65536.0)]
+    s, c, t = np.empty_like(x), np.empty_like(x), np.empty_like(x)
+    lib.nm_sincostan_split_arr(x.ctypes.data, s.ctypes.data, c.ctypes.data, t.ctypes.data, x.size)
+    with np.errstate(all="ignore"):
+        assert_bitwise(s, np.sin(x), x, "split sincostan: sin")
+        assert_bitwise(c, np.cos(x), x, "split sincostan: cos")
+        assert_bitwise(t, np.tan(x), x, "split sincostan: tan")
 
 
 def test_rcp14_restatement(lib):
