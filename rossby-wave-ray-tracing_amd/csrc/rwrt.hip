@@ -1268,19 +1268,36 @@ __device__ __forceinline__ void mercator12(const double g[11], const Merc& M, do
   }
 }
 
+// The wavenumber terms of cal_ugvg and core_diffun: they depend on k and l
+// only, so the RHS forms them beside the trigonometry and the lookup.
+//   kap = l / k, kap^2, 1 + kap^2, k^2 (1 + kap^2), k^2 (1 + kap^2)^2
+// (wn.py:276-281; core_diffun's kap, kap2, kap1, kk and kk * kap1 are the same
+// operations on the same operands, wr.py:53-60).
+struct KapTerms {
+  double kap, kap2, kap1, kk, denom;
+};
+__device__ __forceinline__ KapTerms kap_terms(double k, double l) {
+  KapTerms w;
+  w.kap = RDIV(l, k);
+  w.kap2 = w.kap * w.kap;
+  w.kap1 = 1.0 + w.kap2;
+  w.kk = (k * k) * w.kap1;
+  w.denom = w.kk * w.kap1;
+  return w;
+}
 // cal_ugvg(mode='extent') -> core_cal_ugvg_extent (wn.py:266-294)
 __device__ __forceinline__ void ugvg(double fu, double fv, double fqx, double fqy,
-                                     double k, double l, double& ug, double& vg) {
-  const double kap = RDIV(l, k);
-  const double kap2 = kap * kap;
-  const double kap1 = 1.0 + kap2;
-  const double KK = (k * k) * kap1;
-  const double denom = KK * kap1;
+                                     const KapTerms& w, double& ug, double& vg) {
+  const double kap = w.kap, kap2 = w.kap2, denom = w.denom;
   double qu, qv;
   div2(((1.0 - kap2) * fqy) - ((2.0 * kap) * fqx), denom,
        ((2.0 * kap) * fqy) + ((1.0 - kap2) * fqx), denom, qu, qv);
   ug = fu + qu;
   vg = fv + qv;
+}
+__device__ __forceinline__ void ugvg(double fu, double fv, double fqx, double fqy,
+                                     double k, double l, double& ug, double& vg) {
+  ugvg(fu, fv, fqx, fqy, kap_terms(k, l), ug, vg);
 }
 
 // ---------------------------------------------------------------------------
@@ -1290,6 +1307,9 @@ __device__ __forceinline__ void ugvg(double fu, double fv, double fqx, double fq
 // aux (optional) receives {ug, vg, cos(lat)} of this evaluation -- exactly what
 // the per-interval post-processing recomputes at the same position
 // (wr.py:844, 856-865) -- or NaN for a masked ray (no values computed).
+#ifndef RWRT_KAP_EARLY
+#define RWRT_KAP_EARLY 1
+#endif
 template <class BG>
 __device__ __forceinline__ void ray_rhs(const BG& B, double t, const double* y, double* dy,
                                         double* aux = nullptr) {
@@ -1307,6 +1327,9 @@ __device__ __forceinline__ void ray_rhs(const BG& B, double t, const double* y, 
   const auto trig = np_math::nm_sincostan_begin(lat);
 #endif
   double s, c;
+#if RWRT_KAP_EARLY
+  const KapTerms kw = kap_terms(kx, ky);   // (k, l only: beside the trig and the cell arithmetic)
+#endif
 #if !RWRT_DIAG_NOINTERP
   const auto pending = lookup_begin(B, lon, lat, t);   // the lookup's fill overlaps the trig
 #endif
@@ -1337,20 +1360,20 @@ __device__ __forceinline__ void ray_rhs(const BG& B, double t, const double* y, 
   RWRT_STAMP(4);
   const double fmu = o[0], fmv = o[1], fmux = o[2], fmuy = o[3], fmvx = o[4], fmvy = o[5];
   const double fmqx = o[6], fmqy = o[7], fmqxx = o[8], fmqxy = o[9], fmqyx = o[10], fmqyy = o[11];
+#if !RWRT_KAP_EARLY
+  const KapTerms kw = kap_terms(kx, ky);
+#endif
   double ug, vg;
-  ugvg(fmu, fmv, fmqx, fmqy, kx, ky, ug, vg);
+  ugvg(fmu, fmv, fmqx, fmqy, kw, ug, vg);
   // core_diffun (wr.py:53-78); freq only feeds the dead ps/up terms
-  const double kap = RDIV(ky, kx);
-  const double kap2 = kap * kap;
-  const double kap1 = 1.0 + kap * kap;
-  const double kk = (kx * kx) * kap1;
+  const double kap = kw.kap, kap2 = kw.kap2, kap1 = kw.kap1, kk = kw.kk;
   double qk, ql;
   div2(kap * fmqxx - fmqyx, kk, kap * fmqxy - fmqyy, kk, qk, ql);
   const double dzwn = (-kx) * ((fmux + kap * fmvx) + qk);
   const double dmwn = (-kx) * ((fmuy + kap * fmvy) + ql);
   double damp1, damp2;
   div2(2.0 * ((fmux + fmvy) + kap * (fmvx + fmuy)), kap1,
-       2.0 * (kap * (fmqxx - fmqyy) + (kap2 - 1.0) * fmqxy), kk * kap1, damp1, damp2);
+       2.0 * (kap * (fmqxx - fmqyy) + (kap2 - 1.0) * fmqxy), kw.denom, damp1, damp2);
   const double damp3 = (-2.0 * s) * fmv;
   const double damp = (damp1 + damp2) + damp3;
   div2(ug, kREarth, vg * c, kREarth, dy[0], dy[1]);     // x / R, x / R
@@ -1568,6 +1591,33 @@ __device__ __forceinline__ double stage_input(const KS& K, double t, const doubl
   return t + kCs[S] * h;
 }
 
+// The first J terms of wsum<S> (J < S) for every variable, in wsum's order
+// (more than one variable: sequential in j).
+#ifndef RWRT_STAGE_PARTIAL
+#define RWRT_STAGE_PARTIAL 1
+#endif
+template <int S, int J, int NV, class KS>
+__device__ __forceinline__ void stage_part(const KS& K, const double* f, double* part) {
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    double acc = 0.0;
+#pragma unroll
+    for (int j = 0; j < J; ++j) acc = acc + ((j == 0) ? f[v] : K.get(j, v)) * kW[S][j];
+    part[v] = acc;
+  }
+}
+// The error estimate's terms K0..K5 (dp54_attempt's es without "+ K6 * E6").
+template <int NV, class KS>
+__device__ __forceinline__ void error_part(const KS& K, const double* f, double* part) {
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    double es = 0.0;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) es = es + ((j == 0) ? f[v] : K.get(j, v)) * kE[j];
+    part[v] = es;
+  }
+}
+
 // A problem whose RHS is evaluated by a whole block (rk45_team_kernel) says so
 // with kTeam = true and a stage(s, t, y, dy) member.
 template <class P, class = void>
@@ -1591,6 +1641,59 @@ __device__ __forceinline__ double dp54_attempt(const P& fun, KS& K, double t, co
   double ys[NV], r[NV];
 #ifndef RWRT_UNROLL_STAGES
 #define RWRT_UNROLL_STAGES 1   // six inlined RHS copies: no stage dispatch (the code fits the I-cache)
+#endif
+#if RWRT_STAGE_PARTIAL && RWRT_UNROLL_STAGES
+  if constexpr (NV > 1) {
+    // Each stage's weighted sum is sequential in j and its newest stage comes
+    // last: the terms of the older stages are summed while the current RHS
+    // runs (their LDS reads and dependent adds off the critical path), and
+    // only "+ K_s * w" follows the RHS.  The same operations in the same order
+    // as wsum: bit for bit.
+    double part[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) ys[v] = y[v] + wsum<1, NV>(K, f, v) * h;
+    double ts = t + kCs[1] * h;
+#pragma unroll
+    for (int s = 1; s <= 6; ++s) {
+      switch (s) {   // wave-uniform, compile-time after unrolling
+        case 1: stage_part<2, 1, NV>(K, f, part); break;
+        case 2: stage_part<3, 2, NV>(K, f, part); break;
+        case 3: stage_part<4, 3, NV>(K, f, part); break;
+        case 4: stage_part<5, 4, NV>(K, f, part); break;
+        case 5: stage_part<6, 5, NV>(K, f, part); break;
+        default: error_part<NV>(K, f, part); break;
+      }
+      if constexpr (IsTeam<P>::value) fun.stage(s, ts, ys, r);
+      else fun(ts, ys, r, aux);
+      if (s < 6) {
+        K.put_stage(s, r);
+        const double w = kW[s + 1 < 7 ? s + 1 : 6][s < 6 ? s : 5];
+#pragma unroll
+        for (int v = 0; v < NV; ++v) ys[v] = y[v] + (part[v] + r[v] * w) * h;
+        ts = t + kCs[s + 1 < 7 ? s + 1 : 6] * h;
+      }
+    }
+    double ss = 0.0;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      ynew[v] = ys[v];
+      k6[v] = r[v];
+      const double e = h * (part[v] + r[v] * kE[6]);
+      const double sc = atol + np_max(fabs(y[v]), fabs(ys[v])) * rtol;
+      const double x = e / sc;
+      ss = (v == 0) ? x * x : ss + x * x;
+    }
+    RWRT_STAMP(6);
+    if (Kout) {
+#pragma unroll
+      for (int j = 0; j < 6; ++j)
+#pragma unroll
+        for (int v = 0; v < NV; ++v) Kout[(j * NV + v) * kstride] = (j == 0) ? f[v] : K.get(j, v);
+#pragma unroll
+      for (int v = 0; v < NV; ++v) Kout[(6 * NV + v) * kstride] = r[v];
+    }
+    return sqrt(ss) / RootN<NV>::v;
+  }
 #endif
 #if RWRT_UNROLL_STAGES
 #pragma unroll
