@@ -211,6 +211,9 @@ def main():
                     help="C5: storage of the background levels (arithmetic is fp64 either way)")
     ap.add_argument("--c5-periods", type=int, default=5,
                     help="C5 periods (1-5 of the C3 list; 5 = 9.67 M slots, ~4 M live rays: BASELINE's size)")
+    ap.add_argument("--team", default="0",
+                    help="rays per launch in latency mode (rk45_quad_kernel: four lanes per ray); "
+                         "an integer or 'auto' (RayEngine.team_size)")
     ap.add_argument("--lib", default=None, help="alternative librwrt build (A/B timing)")
     ap.add_argument("--traffic", default=None, help="traffic.json (tools/pmc_traffic.py)")
     ap.add_argument("--valu-profile", default=None, help="valu.json (tools/pmc_valu.py)")
@@ -283,7 +286,8 @@ def main():
         y = make_y0() if gpu_init else y0_d
         return run_sharded(eng, y, nt, 7200.0, group=group, probe=args.probe, lead=lead,
                            chunk=chunk, out=out, events=events, ttotal=(nt - 1) * 7200.0,
-                           order_policy=args.order)
+                           order_policy=args.order,
+                           team=args.team if args.team == "auto" else int(args.team))
 
     for _ in range(args.warmup):
         one_step()
