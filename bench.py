@@ -211,7 +211,7 @@ def main():
                     help="C5: storage of the background levels (arithmetic is fp64 either way)")
     ap.add_argument("--c5-periods", type=int, default=5,
                     help="C5 periods (1-5 of the C3 list; 5 = 9.67 M slots, ~4 M live rays: BASELINE's size)")
-    ap.add_argument("--team", default="0",
+    ap.add_argument("--team", default="auto",
                     help="rays per launch in latency mode (rk45_quad_kernel: four lanes per ray); "
                          "an integer or 'auto' (RayEngine.team_size)")
     ap.add_argument("--lib", default=None, help="alternative librwrt build (A/B timing)")
@@ -337,6 +337,9 @@ def main():
                        "ray_slots": nslot, "live_rays": n_live, "rows": nt,
                        "rows_per_launch": chunk, "launch_rows": schedule,
                        "rank0_rays": n_mine,
+                       "latency_mode": (f"rays above 1.5x the per-lane share of a launch's work run "
+                                        f"in rk45_quad_kernel (four lanes per ray)" if args.team == "auto"
+                                        else f"{args.team} rays per launch in rk45_quad_kernel"),
                        "parallelism": (f"one ray set over {world} GPU(s): cost-balanced split by a "
                                        f"{args.probe}-row probe, RCCL broadcast of the basic state and "
                                        f"gather of endpoints + step counters inside the timed step")},

@@ -2793,6 +2793,8 @@ __global__ void __launch_bounds__(256, 1) rk45_quad_kernel(RunArgs<StaticBG> a) 
   __shared__ __attribute__((aligned(16))) char cache[LaneBG<StaticBG>::kLdsBytes];
   __shared__ double Kq[5 * 2 * 256];
   const CachedStaticBG B = LaneBG<StaticBG>::make(a.B, cache);
+  // above frozen_fill_kernel's waves (priority 0), which may share this CU
+  __builtin_amdgcn_s_setprio(1);
   QuadRole R;
   R.role = threadIdx.x & 3;
   R.odd = (R.role & 1) != 0;

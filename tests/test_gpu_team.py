@@ -1,6 +1,8 @@
-"""Latency mode: rk45_team_kernel (csrc/rwrt.hip), one ray per lane with each
-RHS evaluation split over the four waves (SIMDs) of a block, must give the
-run kernel's results bit for bit.
+"""Latency mode: rk45_quad_kernel (csrc/rwrt.hip; four lanes of a wave per
+ray, the RHS's divisions, stage sums and error norm dealt out over the quad
+and exchanged by DPP) -- or, in a RWRT_LATENCY_QUAD=0 build, rk45_team_kernel
+(each RHS split over the four waves of a block) -- must give the run kernel's
+results bit for bit.
 
 * the C3 cost-stratified sample (tests/golden/c3_sample.npz: the 512 rays
   with the most attempts in day 1 plus rays from 31 cost quantiles) integrated
