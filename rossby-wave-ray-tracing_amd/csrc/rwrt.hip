@@ -2016,7 +2016,7 @@ struct RunArgs {
   double* out;
   int32_t* queue;       // [1]: the work queue's head ([0] unused)
   int64_t n_heavy;      // order[0, n_heavy): rays of rk45_team_kernel (latency mode); the queue is the rest
-  int32_t heavy_blocks; // (unused)
+  int32_t heavy_blocks; // blocks [0, heavy_blocks) run order[0, n_heavy) in latency mode (quad_rays)
   double cut_a;         // haversine argument certainly below cut_off (cal_dis_below)
   const uint8_t* frozen;  // rays frozen at the launch start (NULL: none skipped), see frozen_fill_kernel
 };
@@ -2030,6 +2030,346 @@ inline double haversine_cut(double cut_off) {
   if (!(cut_off > 0.0 && cut_off <= 3.0)) return -1.0;
   const double s = std::sin(0.5 * cut_off);
   return s * s * (1.0 - 1e-9);
+}
+
+// ---------------------------------------------------------------------------
+// Latency mode, v2 (quad_rays, in rk45_run_kernel's first blocks).  Four lanes of one wavefront per ray
+// (a DPP quad, 16 rays per wave): the quad's lanes hold the ray's state
+// replicated and compute the serial parts -- trigonometry, cell arithmetic,
+// lookup, Mercator products, pow, step control -- identically (free on a
+// SIMD), while the parts that are the same instructions on different
+// operands are dealt out over the four lanes (role = lane & 3) and exchanged
+// with quad_perm DPP moves (no LDS, no barrier):
+//   * the RHS's 16 IEEE divisions become two divisions pairs and one
+//     division per lane:
+//       slot 1   role 0: fu/cp, fv/cp       role 1: ux/cp, vx/cp
+//                role 2: cal_ugvg's qu, qv  role 3: core_diffun's qk, ql
+//       slot 2   role 0: damp1, damp2       role 1: dy0, dy1 (ug/R, vg c/R)
+//                role 2: dy2, dy3           (role 3: a copy of role 2)
+//       then     damp * amp / R on every lane;
+//   * the stage sums and the error estimate: lane `role` owns variable `role`
+//     (and every lane variable 4): two sums per lane instead of five, its
+//     stage values K_s (two per stage) in its LDS slice;
+//   * the error norm's five quotients: one pair per lane.
+// Every value is the same operation on the same operands as in ray_rhs /
+// dp54_attempt, so results are the run kernel's bit for bit.  A wave of 16
+// heavy rays also diverges less often (interval ends, cell refills) than one
+// of 64.
+// ---------------------------------------------------------------------------
+#ifndef RWRT_LATENCY_QUAD
+#define RWRT_LATENCY_QUAD 1   // n_heavy rays run in quad_rays (0: rk45_team_kernel)
+#endif
+constexpr int kQuadRays = 64;   // rays per 256-thread block
+
+// x of lane (quad base + P[role]) for every lane of the quad (DPP quad_perm;
+// every lane of a quad is active whenever one is: they share the ray)
+template <int P0, int P1, int P2, int P3>
+__device__ __forceinline__ double qperm(double x) {
+  constexpr int ctrl = P0 | (P1 << 2) | (P2 << 4) | (P3 << 6);
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(x), ctrl, 0xf, 0xf, true);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(x), ctrl, 0xf, 0xf, true);
+  return __hiloint2double(hi, lo);
+}
+template <int J>
+__device__ __forceinline__ double qbcast(double x) { return qperm<J, J, J, J>(x); }
+
+struct QuadRole {
+  int role;
+  bool odd, high;   // role & 1, role & 2
+  __device__ __forceinline__ double sel(double a, double b, double c, double d) const {
+    const double ab = odd ? b : a, cd = odd ? d : c;
+    return high ? cd : ab;
+  }
+};
+
+// ray_rhs (wr.py:492-556) for one ray per quad: returns dy[role] (rA) and
+// dy[4] (rB); aux as in ray_rhs (every lane).
+__device__ __forceinline__ void quad_rhs(const CachedStaticBG& B, const QuadRole& R, const double* y,
+                                         double& rA, double& rB, double* aux) {
+  const double lon = y[0], lat = y[1], kx = y[2];
+  const bool bad = fabs(lat) >= kHalfPi || fabs(y[3]) >= 100.0;
+  const double ky = bad ? kNaN : y[3], amp = y[4];
+  double g[11];
+  const auto trig = np_math::nm_sincostan_begin(lat);
+  const KapTerms kw = kap_terms(kx, ky);
+  const auto pending = lookup_begin(B, lon, lat, 0.0);
+  double s, c, tn;
+  np_math::nm_sincostan_end(lat, trig, s, c, tn);
+  __builtin_amdgcn_sched_barrier(0);
+  lookup_end(B, pending, g);
+  // Mercator (bs.py:856-883): M.cp == c off the pole band; there every
+  // output takes mercator12_masked's extra factor m
+  const Merc M = merc_factors(lat, c, s);
+  const double cp = M.cp, m = M.m;
+  const bool mk = m != 1.0;
+  const double fu = g[F_U], fv = g[F_V];
+  const double fmuy = mk ? (g[F_UY] + tn * fu) * m : g[F_UY] + tn * fu;
+  const double fmvy = mk ? (g[F_VY] + tn * fv) * m : g[F_VY] + tn * fv;
+  const double fmqx = mk ? g[F_QX] * m : g[F_QX];
+  const double fmqy = mk ? (g[F_QY] * cp) * m : g[F_QY] * cp;
+  const double fmqxx = mk ? g[F_QXX] * m : g[F_QXX];
+  const double fmqyx = mk ? (g[F_QXY] * cp) * m : g[F_QXY] * cp;
+  const double fmqxy = mk ? fmqyx * m : fmqyx;
+  const double fmqyy = mk ? (((g[F_QYY] * cp) - (g[F_QY] * M.s)) * cp) * m
+                          : ((g[F_QYY] * cp) - (g[F_QY] * M.s)) * cp;
+  const double kap = kw.kap, kap2 = kw.kap2;
+  // slot 1: the quotients that need no other quotient
+  double q1, q2;
+  {
+    const double n1 = R.sel(fu, g[F_UX], ((1.0 - kap2) * fmqy) - ((2.0 * kap) * fmqx), kap * fmqxx - fmqyx);
+    const double n2 = R.sel(fv, g[F_VX], ((2.0 * kap) * fmqy) + ((1.0 - kap2) * fmqx), kap * fmqxy - fmqyy);
+    const double d = R.sel(cp, cp, kw.denom, kw.kk);
+    div2(n1, d, n2, d, q1, q2);
+  }
+  const double du = qbcast<0>(q1), dv = qbcast<0>(q2), dux = qbcast<1>(q1), dvx = qbcast<1>(q2);
+  const double qu = qbcast<2>(q1), qv = qbcast<2>(q2), qk = qbcast<3>(q1), ql = qbcast<3>(q2);
+  const double fmu = mk ? du * m : du, fmv = mk ? dv * m : dv;
+  const double fmux = mk ? dux * m : dux, fmvx = mk ? dvx * m : dvx;
+  const double ug = fmu + qu, vg = fmv + qv;                       // cal_ugvg (wn.py:266-294)
+  const double dzwn = (-kx) * ((fmux + kap * fmvx) + qk);          // core_diffun (wr.py:53-78)
+  const double dmwn = (-kx) * ((fmuy + kap * fmvy) + ql);
+  // slot 2
+  double p1, p2;
+  {
+    const double a1 = 2.0 * ((fmux + fmvy) + kap * (fmvx + fmuy));
+    const double a2 = 2.0 * (kap * (fmqxx - fmqyy) + (kap2 - 1.0) * fmqxy);
+    const double n1 = R.sel(a1, ug, dzwn, dzwn);
+    const double n2 = R.sel(a2, vg * c, dmwn, dmwn);
+    const bool r0 = !R.odd && !R.high;
+    div2(n1, r0 ? kw.kap1 : kREarth, n2, r0 ? kw.denom : kREarth, p1, p2);
+  }
+  const double damp1 = qbcast<0>(p1), damp2 = qbcast<0>(p2);
+  const double damp = (damp1 + damp2) + (-2.0 * s) * fmv;
+  rB = div_rearth(damp * amp);
+  // dy[role]: dy0, dy1 on role 1, dy2, dy3 on role 2
+  const double a = qperm<1, 1, 2, 2>(p1), b = qperm<1, 1, 2, 2>(p2);
+  rA = R.odd ? b : a;
+  aux[0] = ug;
+  aux[1] = vg;
+  aux[2] = bad ? kNaN : c;
+}
+
+// The stage values K1..K5 this lane owns (variables `role` and 4), in its
+// slice of LDS: element (stage j, slot) at p[((j - 1) * 2 + slot) * 256]
+struct KQuad {
+  double* p;
+  __device__ __forceinline__ double get(int j, int slot) const { return p[((j - 1) * 2 + slot) * 256]; }
+  __device__ __forceinline__ void put(int s, double a, double b) {
+    p[((s - 1) * 2 + 0) * 256] = a;
+    p[((s - 1) * 2 + 1) * 256] = b;
+  }
+};
+// wsum's first J terms of stage S for the owned variables (K0 = fA, fB)
+template <int S, int J>
+__device__ __forceinline__ void quad_part(const KQuad& K, double fA, double fB, double& pA, double& pB) {
+  double a = 0.0, b = 0.0;
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    a = a + ((j == 0) ? fA : K.get(j, 0)) * kW[S][j];
+    b = b + ((j == 0) ? fB : K.get(j, 1)) * kW[S][j];
+  }
+  pA = a;
+  pB = b;
+}
+__device__ __forceinline__ void quad_epart(const KQuad& K, double fA, double fB, double& pA, double& pB) {
+  double a = 0.0, b = 0.0;
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    a = a + ((j == 0) ? fA : K.get(j, 0)) * kE[j];
+    b = b + ((j == 0) ? fB : K.get(j, 1)) * kE[j];
+  }
+  pA = a;
+  pB = b;
+}
+
+// dp54_attempt (rkf45.py:259-321, 368-373) for the quad's ray: fills y_new
+// and K6 (every lane), returns the error norm (every lane)
+__device__ __forceinline__ double quad_attempt(const CachedStaticBG& B, const QuadRole& R, KQuad& K,
+                                               const double* y, const double* f, double h,
+                                               double rtol, double atol, double* ynew, double* k6,
+                                               double* aux) {
+  const double yA = R.sel(y[0], y[1], y[2], y[3]), fA = R.sel(f[0], f[1], f[2], f[3]);
+  const double yB = y[4], fB = f[4];
+  double ys[5];
+#pragma unroll
+  for (int v = 0; v < 5; ++v) ys[v] = y[v] + wsum<1, 5>(K, f, v) * h;   // (K unused for stage 1)
+  double ysA = 0.0, ysB = 0.0, rA = 0.0, rB = 0.0, pA = 0.0, pB = 0.0;
+#pragma unroll
+  for (int s = 1; s <= 6; ++s) {
+    double w = 0.0, cn = 0.0;
+    switch (s) {
+      case 1: quad_part<2, 1>(K, fA, fB, pA, pB); w = kW[2][1]; cn = kCs[2]; break;
+      case 2: quad_part<3, 2>(K, fA, fB, pA, pB); w = kW[3][2]; cn = kCs[3]; break;
+      case 3: quad_part<4, 3>(K, fA, fB, pA, pB); w = kW[4][3]; cn = kCs[4]; break;
+      case 4: quad_part<5, 4>(K, fA, fB, pA, pB); w = kW[5][4]; cn = kCs[5]; break;
+      case 5: quad_part<6, 5>(K, fA, fB, pA, pB); w = kW[6][5]; cn = kCs[6]; break;
+      default: quad_epart(K, fA, fB, pA, pB); break;
+    }
+    (void)cn;   // (autonomous RHS: stage times unused)
+    quad_rhs(B, R, ys, rA, rB, aux);
+    if (s < 6) {
+      K.put(s, rA, rB);
+      ysA = yA + (pA + rA * w) * h;
+      ysB = yB + (pB + rB * w) * h;
+      ys[0] = qbcast<0>(ysA);
+      ys[1] = qbcast<1>(ysA);
+      ys[2] = qbcast<2>(ysA);
+      ys[3] = qbcast<3>(ysA);
+      ys[4] = ysB;
+    }
+  }
+  // ys = y_new, (rA, rB) = K6; error estimate of the owned variables
+#pragma unroll
+  for (int v = 0; v < 5; ++v) ynew[v] = ys[v];
+  k6[0] = qbcast<0>(rA);
+  k6[1] = qbcast<1>(rA);
+  k6[2] = qbcast<2>(rA);
+  k6[3] = qbcast<3>(rA);
+  k6[4] = rB;
+  const double eA = h * (pA + rA * kE[6]), eB = h * (pB + rB * kE[6]);
+  const double scA = atol + np_max(fabs(yA), fabs(ysA)) * rtol;
+  const double scB = atol + np_max(fabs(yB), fabs(ysB)) * rtol;
+  double xA, xB;
+  div2(eA, scA, eB, scB, xA, xB);
+  const double x0 = qbcast<0>(xA), x1 = qbcast<1>(xA), x2 = qbcast<2>(xA), x3 = qbcast<3>(xA);
+  double ss = x0 * x0;
+  ss = ss + x1 * x1;
+  ss = ss + x2 * x2;
+  ss = ss + x3 * x3;
+  ss = ss + xB * xB;
+  return sqrt(ss) / RootN<5>::v;
+}
+
+// Rows [it_begin, it_end) of rays order[0, n_heavy), one per quad (64 per
+// block, no queue): rk45_run_kernel's loop, step control and post-processing.
+// Run by rk45_run_kernel's first a.heavy_blocks blocks (one grid: those
+// blocks are placed with the persistent ones, one per CU, whatever the
+// dispatch order of concurrent kernels), in the run kernel's LDS: the cell
+// cache where the run kernel keeps it, the owned stage values (20 KB) where
+// the run kernel keeps its stages.
+__device__ __forceinline__ void quad_rays(const RunArgs<StaticBG>& a, char* cache, double* Kq) {
+  const CachedStaticBG B = LaneBG<StaticBG>::make(a.B, cache);
+  QuadRole R;
+  R.role = threadIdx.x & 3;
+  R.odd = (R.role & 1) != 0;
+  R.high = (R.role & 2) != 0;
+  KQuad K{Kq + threadIdx.x};
+  const int64_t nrows = a.it_end - a.it_begin;
+  const int64_t w = blockIdx.x * (int64_t)kQuadRays + (threadIdx.x >> 2);
+  const int64_t ray = (w < a.n_heavy) ? a.order[w] : -1;
+  if (ray < 0) return;   // (whole quads: the four lanes share w)
+  double y[5], f[5], aux[3];
+#pragma unroll
+  for (int v = 0; v < 5; ++v) {
+    y[v] = a.state[v * a.nray + ray];
+    f[v] = a.state[(5 + v) * a.nray + ray];
+  }
+  double t = a.state[10 * a.nray + ray], habs = a.state[11 * a.nray + ray], hs = 0.0;
+  int64_t nacc = a.count[2 * ray], nrej = a.count[2 * ray + 1];
+  int32_t nanrow = a.nanrow[ray];
+  int32_t it = a.it_begin;
+  double prev_lon = y[0], prev_lat = y[1], cos_prev = k_cos(prev_lat);
+  aux[2] = kNaN;
+  bool in_step = false, rejected = false;
+  const bool writer = R.role == 0;
+  for (;;) {
+    const double tb = a.tbound[it];
+    // ---- Lane::iterate (rkf45.py:222-253, 375-514)
+    int st = 0;   // 0 step, 1 reached, 2 frozen
+    if (!in_step) {
+      const double sum = (((y[0] + y[1]) + y[2]) + y[3]) + y[4];
+      if (isnan(sum / 5.0)) {
+        t = tb;
+        st = 2;
+      } else if (t == tb) {
+        st = 1;
+      } else {
+        hs = np_max(habs, a.min_step);
+        rejected = false;
+        in_step = true;
+      }
+    }
+    if (st == 0) {
+      double tn = t + hs;
+      if (tn - tb > 0.0) tn = tb;
+      const double h = tn - t;
+      const double ha = fabs(h);
+      double yn[5], k6[5];
+      double en = quad_attempt(B, R, K, y, f, h, a.rtol, a.atol, yn, k6, aux);
+      if (en != en) en = 0.0;
+      const double sp = kSafety * k_pow(en, kErrExp);
+      const bool acc = en < 1.0;
+      double fac = np_min(kMaxFactor, sp);
+      if (en == 0.0) fac = kMaxFactor;
+      if (rejected) fac = np_min(1.0, fac);
+      const double tnew = (tn != tn) ? tb : tn;
+      habs = acc ? ha * fac : habs;
+      hs = acc ? hs : ha * np_max(kMinFactor, sp);
+      t = acc ? tnew : t;
+#pragma unroll
+      for (int v = 0; v < 5; ++v) {
+        y[v] = acc ? yn[v] : y[v];
+        f[v] = acc ? k6[v] : f[v];
+      }
+      in_step = !acc;
+      rejected = rejected || !acc;
+      nacc += acc ? 1 : 0;
+      nrej += acc ? 0 : 1;
+      if (!(acc && t - tb >= 0.0)) continue;
+      st = 1;
+    }
+    // ---- interval it reached: rk45_run_kernel's post-processing (wr.py:835-885)
+    const bool have = !isnan(aux[2]);
+    double ug, vg, cos_c = kNaN;
+    bool masked = fabs(y[1]) >= kHalfPi;
+    if (!masked) {
+      cos_c = have ? aux[2] : cos_small(y[1]);
+      masked = cal_dis_reaches(y[0], y[1], prev_lon, prev_lat, cos_c, cos_prev, a.cut_off, a.cut_a);
+    }
+    if (masked) {
+#pragma unroll
+      for (int v = 0; v < 5; ++v) y[v] = kNaN;
+      ug = vg = kNaN;
+      cos_c = kNaN;
+      aux[2] = kNaN;
+    } else if (have) {
+      ug = aux[0];
+      vg = aux[1];
+    } else {
+      ugvg_at(a.B, tb, y[0], y[1], y[2], y[3], ug, vg);
+    }
+    const int last = (st == 2) ? a.it_end : it + 1;
+    if (writer) {
+      const double2 r0 = make_double2(y[0], y[1]), r1 = make_double2(y[2], y[3]);
+      const double2 r2 = make_double2(y[4], ug), r3 = make_double2(vg, (double)nacc);
+      for (int kr = it; kr < last; ++kr) {
+        double2* o = reinterpret_cast<double2*>(a.out + ((size_t)ray * nrows + (kr - a.it_begin)) * RWRT_NOUT);
+        o[0] = r0;
+        o[1] = r1;
+        o[2] = r2;
+        o[3] = r3;
+      }
+    }
+    if (nanrow == a.nt && isnan(y[0])) nanrow = it;   // wr.py:853-855 (host reduces)
+    prev_lon = y[0];
+    prev_lat = y[1];
+    cos_prev = cos_c;
+    it = last;
+    if (st == 2) t = a.tbound[a.it_end - 1];
+    if (it == a.it_end) break;
+  }
+  if (writer) {
+#pragma unroll
+    for (int v = 0; v < 5; ++v) {
+      a.state[v * a.nray + ray] = y[v];
+      a.state[(5 + v) * a.nray + ray] = f[v];
+    }
+    a.state[10 * a.nray + ray] = t;
+    a.state[11 * a.nray + ray] = habs;
+    a.count[2 * ray] = nacc;
+    a.count[2 * ray + 1] = nrej;
+    a.nanrow[ray] = nanrow;
+  }
 }
 
 // WR.core_ray_run_rk45 (wr.py:767-887) for rows [it_begin, it_end): persistent
@@ -2068,6 +2408,15 @@ __global__ void __launch_bounds__(256, RWRT_WAVES_PER_SIMD) rk45_run_kernel(RunA
   // all LDS in one array: the stages (5 x 5 doubles per lane) then the lookup cache
   constexpr int kKBytes = 5 * 5 * 256 * 8;
   __shared__ __attribute__((aligned(16))) char smem[kKBytes + LaneBG<BG>::kLdsBytes];
+#if RWRT_LATENCY_QUAD
+  if constexpr (std::is_same<BG, StaticBG>::value) {
+    if ((int)blockIdx.x < a.heavy_blocks) {   // (block-uniform) latency mode
+      if (RWRT_RUN_PRIO) __builtin_amdgcn_s_setprio(1);
+      quad_rays(a, smem + kKBytes, reinterpret_cast<double*>(smem));
+      return;
+    }
+  }
+#endif
   const RayProblem P{LaneBG<BG>::make(a.B, smem + kKBytes)};
   const int64_t nrows = a.it_end - a.it_begin;
 #if RWRT_DIAG_STAMPS
@@ -2575,346 +2924,6 @@ __global__ void __launch_bounds__(256, 1) rk45_team_kernel(RunArgs<StaticBG> a) 
       }
       ray = -1;
     }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Latency mode, v2: rk45_quad_kernel.  Four lanes of one wavefront per ray
-// (a DPP quad, 16 rays per wave): the quad's lanes hold the ray's state
-// replicated and compute the serial parts -- trigonometry, cell arithmetic,
-// lookup, Mercator products, pow, step control -- identically (free on a
-// SIMD), while the parts that are the same instructions on different
-// operands are dealt out over the four lanes (role = lane & 3) and exchanged
-// with quad_perm DPP moves (no LDS, no barrier):
-//   * the RHS's 16 IEEE divisions become two divisions pairs and one
-//     division per lane:
-//       slot 1   role 0: fu/cp, fv/cp       role 1: ux/cp, vx/cp
-//                role 2: cal_ugvg's qu, qv  role 3: core_diffun's qk, ql
-//       slot 2   role 0: damp1, damp2       role 1: dy0, dy1 (ug/R, vg c/R)
-//                role 2: dy2, dy3           (role 3: a copy of role 2)
-//       then     damp * amp / R on every lane;
-//   * the stage sums and the error estimate: lane `role` owns variable `role`
-//     (and every lane variable 4): two sums per lane instead of five, its
-//     stage values K_s (two per stage) in its LDS slice;
-//   * the error norm's five quotients: one pair per lane.
-// Every value is the same operation on the same operands as in ray_rhs /
-// dp54_attempt, so results are the run kernel's bit for bit.  A wave of 16
-// heavy rays also diverges less often (interval ends, cell refills) than one
-// of 64.
-// ---------------------------------------------------------------------------
-#ifndef RWRT_LATENCY_QUAD
-#define RWRT_LATENCY_QUAD 1   // n_heavy rays run in rk45_quad_kernel (0: rk45_team_kernel)
-#endif
-constexpr int kQuadRays = 64;   // rays per 256-thread block
-
-// x of lane (quad base + P[role]) for every lane of the quad (DPP quad_perm;
-// every lane of a quad is active whenever one is: they share the ray)
-template <int P0, int P1, int P2, int P3>
-__device__ __forceinline__ double qperm(double x) {
-  constexpr int ctrl = P0 | (P1 << 2) | (P2 << 4) | (P3 << 6);
-  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(x), ctrl, 0xf, 0xf, true);
-  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(x), ctrl, 0xf, 0xf, true);
-  return __hiloint2double(hi, lo);
-}
-template <int J>
-__device__ __forceinline__ double qbcast(double x) { return qperm<J, J, J, J>(x); }
-
-struct QuadRole {
-  int role;
-  bool odd, high;   // role & 1, role & 2
-  __device__ __forceinline__ double sel(double a, double b, double c, double d) const {
-    const double ab = odd ? b : a, cd = odd ? d : c;
-    return high ? cd : ab;
-  }
-};
-
-// ray_rhs (wr.py:492-556) for one ray per quad: returns dy[role] (rA) and
-// dy[4] (rB); aux as in ray_rhs (every lane).
-__device__ __forceinline__ void quad_rhs(const CachedStaticBG& B, const QuadRole& R, const double* y,
-                                         double& rA, double& rB, double* aux) {
-  const double lon = y[0], lat = y[1], kx = y[2];
-  const bool bad = fabs(lat) >= kHalfPi || fabs(y[3]) >= 100.0;
-  const double ky = bad ? kNaN : y[3], amp = y[4];
-  double g[11];
-  const auto trig = np_math::nm_sincostan_begin(lat);
-  const KapTerms kw = kap_terms(kx, ky);
-  const auto pending = lookup_begin(B, lon, lat, 0.0);
-  double s, c, tn;
-  np_math::nm_sincostan_end(lat, trig, s, c, tn);
-  __builtin_amdgcn_sched_barrier(0);
-  lookup_end(B, pending, g);
-  // Mercator (bs.py:856-883): M.cp == c off the pole band; there every
-  // output takes mercator12_masked's extra factor m
-  const Merc M = merc_factors(lat, c, s);
-  const double cp = M.cp, m = M.m;
-  const bool mk = m != 1.0;
-  const double fu = g[F_U], fv = g[F_V];
-  const double fmuy = mk ? (g[F_UY] + tn * fu) * m : g[F_UY] + tn * fu;
-  const double fmvy = mk ? (g[F_VY] + tn * fv) * m : g[F_VY] + tn * fv;
-  const double fmqx = mk ? g[F_QX] * m : g[F_QX];
-  const double fmqy = mk ? (g[F_QY] * cp) * m : g[F_QY] * cp;
-  const double fmqxx = mk ? g[F_QXX] * m : g[F_QXX];
-  const double fmqyx = mk ? (g[F_QXY] * cp) * m : g[F_QXY] * cp;
-  const double fmqxy = mk ? fmqyx * m : fmqyx;
-  const double fmqyy = mk ? (((g[F_QYY] * cp) - (g[F_QY] * M.s)) * cp) * m
-                          : ((g[F_QYY] * cp) - (g[F_QY] * M.s)) * cp;
-  const double kap = kw.kap, kap2 = kw.kap2;
-  // slot 1: the quotients that need no other quotient
-  double q1, q2;
-  {
-    const double n1 = R.sel(fu, g[F_UX], ((1.0 - kap2) * fmqy) - ((2.0 * kap) * fmqx), kap * fmqxx - fmqyx);
-    const double n2 = R.sel(fv, g[F_VX], ((2.0 * kap) * fmqy) + ((1.0 - kap2) * fmqx), kap * fmqxy - fmqyy);
-    const double d = R.sel(cp, cp, kw.denom, kw.kk);
-    div2(n1, d, n2, d, q1, q2);
-  }
-  const double du = qbcast<0>(q1), dv = qbcast<0>(q2), dux = qbcast<1>(q1), dvx = qbcast<1>(q2);
-  const double qu = qbcast<2>(q1), qv = qbcast<2>(q2), qk = qbcast<3>(q1), ql = qbcast<3>(q2);
-  const double fmu = mk ? du * m : du, fmv = mk ? dv * m : dv;
-  const double fmux = mk ? dux * m : dux, fmvx = mk ? dvx * m : dvx;
-  const double ug = fmu + qu, vg = fmv + qv;                       // cal_ugvg (wn.py:266-294)
-  const double dzwn = (-kx) * ((fmux + kap * fmvx) + qk);          // core_diffun (wr.py:53-78)
-  const double dmwn = (-kx) * ((fmuy + kap * fmvy) + ql);
-  // slot 2
-  double p1, p2;
-  {
-    const double a1 = 2.0 * ((fmux + fmvy) + kap * (fmvx + fmuy));
-    const double a2 = 2.0 * (kap * (fmqxx - fmqyy) + (kap2 - 1.0) * fmqxy);
-    const double n1 = R.sel(a1, ug, dzwn, dzwn);
-    const double n2 = R.sel(a2, vg * c, dmwn, dmwn);
-    const bool r0 = !R.odd && !R.high;
-    div2(n1, r0 ? kw.kap1 : kREarth, n2, r0 ? kw.denom : kREarth, p1, p2);
-  }
-  const double damp1 = qbcast<0>(p1), damp2 = qbcast<0>(p2);
-  const double damp = (damp1 + damp2) + (-2.0 * s) * fmv;
-  rB = div_rearth(damp * amp);
-  // dy[role]: dy0, dy1 on role 1, dy2, dy3 on role 2
-  const double a = qperm<1, 1, 2, 2>(p1), b = qperm<1, 1, 2, 2>(p2);
-  rA = R.odd ? b : a;
-  aux[0] = ug;
-  aux[1] = vg;
-  aux[2] = bad ? kNaN : c;
-}
-
-// The stage values K1..K5 this lane owns (variables `role` and 4), in its
-// slice of LDS: element (stage j, slot) at p[((j - 1) * 2 + slot) * 256]
-struct KQuad {
-  double* p;
-  __device__ __forceinline__ double get(int j, int slot) const { return p[((j - 1) * 2 + slot) * 256]; }
-  __device__ __forceinline__ void put(int s, double a, double b) {
-    p[((s - 1) * 2 + 0) * 256] = a;
-    p[((s - 1) * 2 + 1) * 256] = b;
-  }
-};
-// wsum's first J terms of stage S for the owned variables (K0 = fA, fB)
-template <int S, int J>
-__device__ __forceinline__ void quad_part(const KQuad& K, double fA, double fB, double& pA, double& pB) {
-  double a = 0.0, b = 0.0;
-#pragma unroll
-  for (int j = 0; j < J; ++j) {
-    a = a + ((j == 0) ? fA : K.get(j, 0)) * kW[S][j];
-    b = b + ((j == 0) ? fB : K.get(j, 1)) * kW[S][j];
-  }
-  pA = a;
-  pB = b;
-}
-__device__ __forceinline__ void quad_epart(const KQuad& K, double fA, double fB, double& pA, double& pB) {
-  double a = 0.0, b = 0.0;
-#pragma unroll
-  for (int j = 0; j < 6; ++j) {
-    a = a + ((j == 0) ? fA : K.get(j, 0)) * kE[j];
-    b = b + ((j == 0) ? fB : K.get(j, 1)) * kE[j];
-  }
-  pA = a;
-  pB = b;
-}
-
-// dp54_attempt (rkf45.py:259-321, 368-373) for the quad's ray: fills y_new
-// and K6 (every lane), returns the error norm (every lane)
-__device__ __forceinline__ double quad_attempt(const CachedStaticBG& B, const QuadRole& R, KQuad& K,
-                                               const double* y, const double* f, double h,
-                                               double rtol, double atol, double* ynew, double* k6,
-                                               double* aux) {
-  const double yA = R.sel(y[0], y[1], y[2], y[3]), fA = R.sel(f[0], f[1], f[2], f[3]);
-  const double yB = y[4], fB = f[4];
-  double ys[5];
-#pragma unroll
-  for (int v = 0; v < 5; ++v) ys[v] = y[v] + wsum<1, 5>(K, f, v) * h;   // (K unused for stage 1)
-  double ysA = 0.0, ysB = 0.0, rA = 0.0, rB = 0.0, pA = 0.0, pB = 0.0;
-#pragma unroll
-  for (int s = 1; s <= 6; ++s) {
-    double w = 0.0, cn = 0.0;
-    switch (s) {
-      case 1: quad_part<2, 1>(K, fA, fB, pA, pB); w = kW[2][1]; cn = kCs[2]; break;
-      case 2: quad_part<3, 2>(K, fA, fB, pA, pB); w = kW[3][2]; cn = kCs[3]; break;
-      case 3: quad_part<4, 3>(K, fA, fB, pA, pB); w = kW[4][3]; cn = kCs[4]; break;
-      case 4: quad_part<5, 4>(K, fA, fB, pA, pB); w = kW[5][4]; cn = kCs[5]; break;
-      case 5: quad_part<6, 5>(K, fA, fB, pA, pB); w = kW[6][5]; cn = kCs[6]; break;
-      default: quad_epart(K, fA, fB, pA, pB); break;
-    }
-    (void)cn;   // (autonomous RHS: stage times unused)
-    quad_rhs(B, R, ys, rA, rB, aux);
-    if (s < 6) {
-      K.put(s, rA, rB);
-      ysA = yA + (pA + rA * w) * h;
-      ysB = yB + (pB + rB * w) * h;
-      ys[0] = qbcast<0>(ysA);
-      ys[1] = qbcast<1>(ysA);
-      ys[2] = qbcast<2>(ysA);
-      ys[3] = qbcast<3>(ysA);
-      ys[4] = ysB;
-    }
-  }
-  // ys = y_new, (rA, rB) = K6; error estimate of the owned variables
-#pragma unroll
-  for (int v = 0; v < 5; ++v) ynew[v] = ys[v];
-  k6[0] = qbcast<0>(rA);
-  k6[1] = qbcast<1>(rA);
-  k6[2] = qbcast<2>(rA);
-  k6[3] = qbcast<3>(rA);
-  k6[4] = rB;
-  const double eA = h * (pA + rA * kE[6]), eB = h * (pB + rB * kE[6]);
-  const double scA = atol + np_max(fabs(yA), fabs(ysA)) * rtol;
-  const double scB = atol + np_max(fabs(yB), fabs(ysB)) * rtol;
-  double xA, xB;
-  div2(eA, scA, eB, scB, xA, xB);
-  const double x0 = qbcast<0>(xA), x1 = qbcast<1>(xA), x2 = qbcast<2>(xA), x3 = qbcast<3>(xA);
-  double ss = x0 * x0;
-  ss = ss + x1 * x1;
-  ss = ss + x2 * x2;
-  ss = ss + x3 * x3;
-  ss = ss + xB * xB;
-  return sqrt(ss) / RootN<5>::v;
-}
-
-// rows [it_begin, it_end) of rays order[0, n_heavy), one per quad (64 per
-// block, no queue); rk45_run_kernel's loop, step control and post-processing
-__global__ void __launch_bounds__(256, 1) rk45_quad_kernel(RunArgs<StaticBG> a) {
-  nm_stage<NM_ALL>();
-  __shared__ __attribute__((aligned(16))) char cache[LaneBG<StaticBG>::kLdsBytes];
-  __shared__ double Kq[5 * 2 * 256];
-  const CachedStaticBG B = LaneBG<StaticBG>::make(a.B, cache);
-  // above frozen_fill_kernel's waves (priority 0), which may share this CU
-  __builtin_amdgcn_s_setprio(1);
-  QuadRole R;
-  R.role = threadIdx.x & 3;
-  R.odd = (R.role & 1) != 0;
-  R.high = (R.role & 2) != 0;
-  KQuad K{Kq + threadIdx.x};
-  const int64_t nrows = a.it_end - a.it_begin;
-  const int64_t w = blockIdx.x * (int64_t)kQuadRays + (threadIdx.x >> 2);
-  const int64_t ray = (w < a.n_heavy) ? a.order[w] : -1;
-  if (ray < 0) return;   // (whole quads: the four lanes share w)
-  double y[5], f[5], aux[3];
-#pragma unroll
-  for (int v = 0; v < 5; ++v) {
-    y[v] = a.state[v * a.nray + ray];
-    f[v] = a.state[(5 + v) * a.nray + ray];
-  }
-  double t = a.state[10 * a.nray + ray], habs = a.state[11 * a.nray + ray], hs = 0.0;
-  int64_t nacc = a.count[2 * ray], nrej = a.count[2 * ray + 1];
-  int32_t nanrow = a.nanrow[ray];
-  int32_t it = a.it_begin;
-  double prev_lon = y[0], prev_lat = y[1], cos_prev = k_cos(prev_lat);
-  aux[2] = kNaN;
-  bool in_step = false, rejected = false;
-  const bool writer = R.role == 0;
-  for (;;) {
-    const double tb = a.tbound[it];
-    // ---- Lane::iterate (rkf45.py:222-253, 375-514)
-    int st = 0;   // 0 step, 1 reached, 2 frozen
-    if (!in_step) {
-      const double sum = (((y[0] + y[1]) + y[2]) + y[3]) + y[4];
-      if (isnan(sum / 5.0)) {
-        t = tb;
-        st = 2;
-      } else if (t == tb) {
-        st = 1;
-      } else {
-        hs = np_max(habs, a.min_step);
-        rejected = false;
-        in_step = true;
-      }
-    }
-    if (st == 0) {
-      double tn = t + hs;
-      if (tn - tb > 0.0) tn = tb;
-      const double h = tn - t;
-      const double ha = fabs(h);
-      double yn[5], k6[5];
-      double en = quad_attempt(B, R, K, y, f, h, a.rtol, a.atol, yn, k6, aux);
-      if (en != en) en = 0.0;
-      const double sp = kSafety * k_pow(en, kErrExp);
-      const bool acc = en < 1.0;
-      double fac = np_min(kMaxFactor, sp);
-      if (en == 0.0) fac = kMaxFactor;
-      if (rejected) fac = np_min(1.0, fac);
-      const double tnew = (tn != tn) ? tb : tn;
-      habs = acc ? ha * fac : habs;
-      hs = acc ? hs : ha * np_max(kMinFactor, sp);
-      t = acc ? tnew : t;
-#pragma unroll
-      for (int v = 0; v < 5; ++v) {
-        y[v] = acc ? yn[v] : y[v];
-        f[v] = acc ? k6[v] : f[v];
-      }
-      in_step = !acc;
-      rejected = rejected || !acc;
-      nacc += acc ? 1 : 0;
-      nrej += acc ? 0 : 1;
-      if (!(acc && t - tb >= 0.0)) continue;
-      st = 1;
-    }
-    // ---- interval it reached: rk45_run_kernel's post-processing (wr.py:835-885)
-    const bool have = !isnan(aux[2]);
-    double ug, vg, cos_c = kNaN;
-    bool masked = fabs(y[1]) >= kHalfPi;
-    if (!masked) {
-      cos_c = have ? aux[2] : cos_small(y[1]);
-      masked = cal_dis_reaches(y[0], y[1], prev_lon, prev_lat, cos_c, cos_prev, a.cut_off, a.cut_a);
-    }
-    if (masked) {
-#pragma unroll
-      for (int v = 0; v < 5; ++v) y[v] = kNaN;
-      ug = vg = kNaN;
-      cos_c = kNaN;
-      aux[2] = kNaN;
-    } else if (have) {
-      ug = aux[0];
-      vg = aux[1];
-    } else {
-      ugvg_at(a.B, tb, y[0], y[1], y[2], y[3], ug, vg);
-    }
-    const int last = (st == 2) ? a.it_end : it + 1;
-    if (writer) {
-      const double2 r0 = make_double2(y[0], y[1]), r1 = make_double2(y[2], y[3]);
-      const double2 r2 = make_double2(y[4], ug), r3 = make_double2(vg, (double)nacc);
-      for (int kr = it; kr < last; ++kr) {
-        double2* o = reinterpret_cast<double2*>(a.out + ((size_t)ray * nrows + (kr - a.it_begin)) * RWRT_NOUT);
-        o[0] = r0;
-        o[1] = r1;
-        o[2] = r2;
-        o[3] = r3;
-      }
-    }
-    if (nanrow == a.nt && isnan(y[0])) nanrow = it;   // wr.py:853-855 (host reduces)
-    prev_lon = y[0];
-    prev_lat = y[1];
-    cos_prev = cos_c;
-    it = last;
-    if (st == 2) t = a.tbound[a.it_end - 1];
-    if (it == a.it_end) break;
-  }
-  if (writer) {
-#pragma unroll
-    for (int v = 0; v < 5; ++v) {
-      a.state[v * a.nray + ray] = y[v];
-      a.state[(5 + v) * a.nray + ray] = f[v];
-    }
-    a.state[10 * a.nray + ray] = t;
-    a.state[11 * a.nray + ray] = habs;
-    a.count[2 * ray] = nacc;
-    a.count[2 * ray + 1] = nrej;
-    a.nanrow[ray] = nanrow;
   }
 }
 
@@ -3495,19 +3504,26 @@ rwrt_status launch_run(rwrt_ctx* ctx, const BG& B, int64_t nray, const rwrt_para
       }))
     return s;
 #endif
+#if RWRT_LATENCY_QUAD
+  // latency mode in the run kernel's first team_blocks blocks (quad_rays):
+  // one grid, so they are placed beside the persistent blocks whatever the
+  // hardware queues' dispatch order (a second kernel on another stream could
+  // wait for a CU on its XCD until the persistent grid drains)
+  a.heavy_blocks = (int32_t)team_blocks;
+  if (nray > n_heavy || team_blocks) {
+    const int64_t grid = team_blocks + (nray > n_heavy ? blocks : 0);
+    hipLaunchKernelGGL(rk45_run_kernel<BG>, dim3((unsigned)grid), dim3(256), 0, st, a);
+    if (rwrt_status s = check_launch("rk45_run_kernel")) return s;
+  }
+#else
   if (team_blocks) {
     // latency mode on the context's team stream, after the flags (and
     // everything before this call on `stream`); `stream` waits for it below
     if (hipEventRecord(ctx->team_go, st) != hipSuccess || hipStreamWaitEvent(ctx->team, ctx->team_go, 0) != hipSuccess)
       return check_launch("hipEventRecord(latency mode start)");
     if constexpr (std::is_same<BG, StaticBG>::value) {
-#if RWRT_LATENCY_QUAD
-      hipLaunchKernelGGL(rk45_quad_kernel, dim3((unsigned)team_blocks), dim3(256), 0, ctx->team, a);
-      if (rwrt_status s = check_launch("rk45_quad_kernel")) return s;
-#else
       hipLaunchKernelGGL(rk45_team_kernel, dim3((unsigned)team_blocks), dim3(256), 0, ctx->team, a);
       if (rwrt_status s = check_launch("rk45_team_kernel")) return s;
-#endif
     }
     if (hipEventRecord(ctx->team_end, ctx->team) != hipSuccess)
       return check_launch("hipEventRecord(latency mode end)");
@@ -3518,6 +3534,7 @@ rwrt_status launch_run(rwrt_ctx* ctx, const BG& B, int64_t nray, const rwrt_para
   }
   if (team_blocks && hipStreamWaitEvent(st, ctx->team_end, 0) != hipSuccess)
     return check_launch("hipStreamWaitEvent(latency mode end)");
+#endif
 #if RWRT_FROZEN_FILL
 #ifndef RWRT_DIAG_FILL
 #define RWRT_DIAG_FILL 0   // timing-only diagnostic builds: 1 = no fill launch, 2 = the fill after the run kernel

@@ -5,6 +5,8 @@ drive.  It owns the packed field stack on the GPU and wraps every C-ABI call
 of ``include/rwrt.h``; ``integrate`` is the whole ray loop of the reference's
 ``WR.core_ray_run_rk45`` (wr.py:767-887), streamed in time chunks.
 """
+import os
+
 import numpy as np
 import torch
 
@@ -269,16 +271,20 @@ class RayEngine:
         key = torch.where(frozen, torch.full_like(work, -1), work)
         return torch.sort(key, descending=True, stable=True).indices.to(torch.int64).contiguous()
 
+    # a heavy ray's attempt in rk45_quad_kernel / in a loaded rk45_run_kernel
+    # wave (tools/team_latency.py: 11.5 vs 13.3-13.7 us on the heaviest C3 rays)
+    QUAD_ATTEMPT_RATIO = 0.85
+    QUAD_MIN_GAIN = 0.07
+
     def team_capacity(self):
         """Rays the latency mode takes at most (64 per CU, half the CUs)."""
         return (torch.cuda.get_device_properties(self.device).multi_processor_count // 2) * 64
 
     def team_size(self, team, st, work, order, rows):
         """How many of the first rays of ``order`` (live at the launch start)
-        go to the latency mode.  An int asks for that many; "auto" takes the
-        rays whose previous-launch work exceeds the launch's fair share per
-        lane (the total over the persistent lanes), which would otherwise
-        outlast the rest."""
+        go to the latency mode.  An int asks for that many; "auto" picks the
+        number that minimises the launch's predicted makespan from each ray's
+        previous-launch work (below)."""
         if order is None or self.bg is not None:   # (the latency mode is static-background only)
             return 0
         live = ~torch.isnan(st["state"][:5].sum(0))
@@ -288,13 +294,28 @@ class RayEngine:
             n = min(int(team), cap)
             # the first n entries of the order must be live rays
             return n if n == 0 or bool(live[order[:n]].all()) else 0
-        if work is None:
+        if work is None or cap < 1:
             return 0
-        w = torch.where(live, work, torch.zeros_like(work))
-        lanes = torch.cuda.get_device_properties(self.device).multi_processor_count * 256
-        share = float(w.sum().item()) / lanes
-        n = int((w > 1.5 * share).sum().item())
-        return min(n, cap)
+        # predicted makespan of the launch for n heavy rays in latency mode (n a
+        # multiple of its 64 rays per block, each block taking a CU from the
+        # run kernel's persistent grid), in run-kernel attempt times:
+        #   max(heaviest ray x QUAD_ATTEMPT_RATIO,             (latency mode)
+        #       ray n+1, remaining work / remaining lanes)     (run kernel)
+        # and the n that minimises it (the smallest on ties)
+        w = torch.where(live, work, torch.zeros_like(work))[order].to(torch.float64)
+        ncu = torch.cuda.get_device_properties(self.device).multi_processor_count
+        cum = torch.cumsum(w, 0)
+        n = torch.arange(0, cap + 1, 64, device=w.device)
+        n = torch.unique(torch.cat([n, torch.tensor([cap], device=w.device)]))
+        rest = cum[-1] - torch.where(n > 0, cum[(n - 1).clamp(min=0)], torch.zeros_like(cum[:1]))
+        lanes = 256.0 * (ncu - (n + 63) // 64).clamp(min=1)
+        nxt = torch.where(n < w.numel(), w[n.clamp(max=w.numel() - 1)], torch.zeros_like(rest))
+        t = torch.maximum(torch.maximum(nxt, rest / lanes),
+                          torch.where(n > 0, w[0] * self.QUAD_ATTEMPT_RATIO, torch.zeros_like(rest)))
+        # (the prediction ignores what the split costs beyond the CUs: take the
+        # latency mode only for a predicted gain of QUAD_MIN_GAIN or more)
+        k = int(torch.argmin(t).item())
+        return int(n[k].item()) if float(t[k]) <= (1.0 - self.QUAD_MIN_GAIN) * float(t[0]) else 0
 
     def run(self, st, p, tbound, it_begin, it_end, out, order=None, n_heavy=0):
         """Rows ``[it_begin, it_end)`` into ``out[nray, it_end-it_begin, 8]`` (async)."""
@@ -440,6 +461,8 @@ class RayEngine:
                 work = cnt.sum(1) - prev_work
                 order = self.cost_order(st, work)
             n_heavy = self.team_size(team, st, work, order, i1 - i0) if team else 0
+            if os.environ.get("RWRT_DEBUG_TEAM"):
+                print(f"launch rows [{i0}, {i1}): n_heavy {n_heavy}", flush=True)
             prev_work = cnt.sum(1)
             if events is not None:
                 e0, e1, es = self._event_pair()
