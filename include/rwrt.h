@@ -165,9 +165,11 @@ rwrt_status rwrt_rk45_init(const rwrt_grid* g, const double* d_packed,
  * to d_tbound[i] (t_eval, wr.py:798-801) with the reference's step control
  * (rkf45.py:222-253,375-514), then masked (wr.py:838-850) and its group
  * velocity recomputed (wr.py:856-865).  Rays are taken from device work
- * queues in the order d_order[nray] (NULL = 0..nray-1): the first n_heavy
- * entries are served first by one high-priority wave per SIMD (pass the
- * rays expected to be slowest there; 0 = a single queue).  Output row r of
+ * queues in the order d_order[nray] (NULL = 0..nray-1); the first n_heavy
+ * entries (live rays, static background only, at most 64 per CU on half the
+ * CUs) run in latency mode -- four lanes of a wave per ray, in the first
+ * blocks of the same grid (pass the rays expected to be slowest; 0 = none).
+ * Output row r of
  * ray j is d_out[(j*(it_end-it_begin) + r)*8 + {lon,lat,k,l,amp,ug,vg,nacc}].
  * d_state / d_count / d_nanrow carry the per-ray solver state across calls
  * (time chunking).  d_work: >= 2 int32 of scratch (queue heads), reset by

@@ -44,19 +44,21 @@ def main():
     ap.add_argument("--worlds", default="1,2,4,8")
     ap.add_argument("--out", default=None)
     ap.add_argument("--bg", default="zonal", choices=["zonal", "nonzonal"])
-    ap.add_argument("--team", default="0", help="latency-mode rays per launch (int or 'auto')")
+    ap.add_argument("--team", default="auto", help="latency-mode rays per launch (int or 'auto')")
+    ap.add_argument("--lead", default="24,96", help="rows of the re-ordering launches after the probe")
     a = ap.parse_args()
     team = a.team if a.team == "auto" else int(a.team)
+    lead = [int(x) for x in a.lead.split(",") if x]
     bs, bg = bench.make_bs(a.bg)
     y0 = torch.as_tensor(bench.c3_initial_state(bs), device="cuda")
     eng = RayEngine.from_bs(bs)
     nt = int(a.days * 12) + 1
-    out = {"days": a.days, "bg": a.bg, "team": a.team, "worlds": {}}
+    out = {"days": a.days, "bg": a.bg, "team": a.team, "lead": a.lead, "worlds": {}}
     for w in [int(x) for x in a.worlds.split(",")]:
         ranks = []
         for r in range(w):
             dt, res = timed(lambda: run_sharded(eng, y0, nt, rank=r, world=w, gather=False,
-                                                       team=team))
+                                                       team=team, lead=lead))
             ranks.append({"rank": r, "s": dt, "rays": int(res.idx.numel()), "ray_steps": res.steps_local,
                           "max_attempts": int((res.res.nacc + res.res.nrej).max().item())})
         steps = sum(x["ray_steps"] for x in ranks)
