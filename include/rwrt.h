@@ -92,6 +92,12 @@ const char* rwrt_version(void);
 typedef struct rwrt_ctx rwrt_ctx;
 rwrt_status rwrt_ctx_create(int32_t device, rwrt_ctx** out);
 rwrt_status rwrt_ctx_destroy(rwrt_ctx* ctx);
+/* Rays per wavefront in the latency mode of rwrt_rk45_run (n_heavy > 0) on
+ * this context: 1..16 (default 16 = 64 rays per CU).  Fewer rays per wave
+ * make each heavy ray's attempts faster (its wave stalls less often on the
+ * other rays' cell refills and interval ends) at more CUs per heavy ray.
+ * Schedule only: results do not depend on it. */
+rwrt_status rwrt_ctx_set_latency_density(rwrt_ctx* ctx, int32_t rays_per_wave);
 /* Last error message of the calling thread ("" if none). */
 const char* rwrt_last_error(void);
 

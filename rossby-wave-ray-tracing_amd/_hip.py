@@ -14,6 +14,7 @@ LIB_PATH = os.environ.get("RWRT_LIB", os.path.join(_HERE, "librwrt.so"))
 
 NFIELD_REF, NFIELD_PACK, NVAR, NMERC, NOUT, NSTATE = 18, 12, 5, 12, 8, 12
 ABI_SYMBOLS = ("rwrt_version", "rwrt_last_error", "rwrt_ctx_create", "rwrt_ctx_destroy",
+               "rwrt_ctx_set_latency_density",
                "rwrt_pack_fields",
                "rwrt_mercator_point", "rwrt_rhs", "rwrt_dp54_attempt",
                "rwrt_ray_initial", "rwrt_rk45_init", "rwrt_rk45_run", "rwrt_rk4_run",
@@ -82,6 +83,7 @@ def load():
         "rwrt_rk45_run_tv": [_P, G, B, _I64, Pr, _P, _I32, _I32, _P, _I64, _P, _P, _P, _P, _P, _P],
         "rwrt_ctx_create": [_I32, ctypes.POINTER(_P)],
         "rwrt_ctx_destroy": [_P],
+        "rwrt_ctx_set_latency_density": [_P, _I32],
         "rwrt_rhs_tv": [G, B, _I64, _P, _P, _P, _P],
         "rwrt_kat_rk45": [_I32, _I64, _P, _I32, _P, _D, _D, _D, _P, _P],
         "rwrt_selftest_math": [_I32, _I64, _P, _P, _P, _P],
@@ -144,6 +146,12 @@ class Context:
     @property
     def handle(self):
         return self._h
+
+    def set_latency_density(self, rays_per_wave):
+        """Rays per wave in the latency mode (1..16): rwrt_ctx_set_latency_density."""
+        if getattr(self, "_qpw", 16) != int(rays_per_wave):
+            check(load().rwrt_ctx_set_latency_density(self._h, int(rays_per_wave)))
+            self._qpw = int(rays_per_wave)
 
     def close(self):
         h, self._h = getattr(self, "_h", None), None

@@ -2019,6 +2019,7 @@ struct RunArgs {
   int32_t heavy_blocks; // blocks [0, heavy_blocks) run order[0, n_heavy) in latency mode (quad_rays)
   double cut_a;         // haversine argument certainly below cut_off (cal_dis_below)
   const uint8_t* frozen;  // rays frozen at the launch start (NULL: none skipped), see frozen_fill_kernel
+  int32_t quad_per_wave = 16;  // latency mode: rays per wave (1..16; fewer = less divergence per ray)
 };
 
 // Haversine threshold: d = 2 atan2(sqrt(a), sqrt(1 - a)) increases with a, so
@@ -2059,7 +2060,6 @@ inline double haversine_cut(double cut_off) {
 #ifndef RWRT_LATENCY_QUAD
 #define RWRT_LATENCY_QUAD 1   // n_heavy rays run in quad_rays (0: rk45_team_kernel)
 #endif
-constexpr int kQuadRays = 64;   // rays per 256-thread block
 
 // x of lane (quad base + P[role]) for every lane of the quad (DPP quad_perm;
 // every lane of a quad is active whenever one is: they share the ray)
@@ -2255,8 +2255,12 @@ __device__ __forceinline__ void quad_rays(const RunArgs<StaticBG>& a, char* cach
   R.high = (R.role & 2) != 0;
   KQuad K{Kq + threadIdx.x};
   const int64_t nrows = a.it_end - a.it_begin;
-  const int64_t w = blockIdx.x * (int64_t)kQuadRays + (threadIdx.x >> 2);
-  const int64_t ray = (w < a.n_heavy) ? a.order[w] : -1;
+  // order position of this quad's ray: the heaviest rays one per wave first
+  // (position p -> wave p % waves, quad p / waves), a.quad_per_wave quads per wave
+  const int qi = (threadIdx.x & 63) >> 2;
+  const int64_t waves = 4 * (int64_t)a.heavy_blocks;
+  const int64_t w = qi * waves + blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t ray = (qi < a.quad_per_wave && w < a.n_heavy) ? a.order[w] : -1;
   if (ray < 0) return;   // (whole quads: the four lanes share w)
   double y[5], f[5], aux[3];
 #pragma unroll
@@ -3379,6 +3383,7 @@ struct rwrt_ctx {
   hipStream_t team = nullptr;   // rk45_team_kernel (latency mode)
   hipEvent_t flagged = nullptr, filled = nullptr, team_go = nullptr, team_end = nullptr;
   hipEvent_t done = nullptr;   // end of the last call on this context
+  int quad_per_wave = 16;      // latency mode: rays per wave (rwrt_ctx_set_latency_density)
   bool used = false;
   std::mutex mu;
 };
@@ -3474,9 +3479,14 @@ rwrt_status launch_run(rwrt_ctx* ctx, const BG& B, int64_t nray, const rwrt_para
   if (n_heavy > 0 && !d_order) return fail(RWRT_ERR_ARG, "n_heavy > 0 needs d_order%s");
   if (n_heavy > 0 && !std::is_same<BG, StaticBG>::value)
     return fail(RWRT_ERR_ARG, "latency mode (n_heavy > 0) runs on the static background only%s");
-  const int64_t team_blocks = (n_heavy + kTeamLanes - 1) / kTeamLanes;
+#if RWRT_LATENCY_QUAD
+  const int64_t per_block = 4 * (int64_t)ctx->quad_per_wave;   // rays per latency-mode block
+#else
+  const int64_t per_block = kTeamLanes;
+#endif
+  const int64_t team_blocks = (n_heavy + per_block - 1) / per_block;
   if (team_blocks > ctx->ncu / 2)
-    return fail(RWRT_ERR_ARG, "n_heavy exceeds the latency mode's capacity (64 rays per CU, half the CUs)%s");
+    return fail(RWRT_ERR_ARG, "n_heavy exceeds the latency mode's capacity (4 x rays-per-wave per CU, half the CUs)%s");
   std::lock_guard<std::mutex> lock(ctx->mu);
   DeviceGuard dg(ctx->device);
   if (!dg.ok) return check_launch("hipSetDevice(context device)");
@@ -3510,6 +3520,7 @@ rwrt_status launch_run(rwrt_ctx* ctx, const BG& B, int64_t nray, const rwrt_para
   // hardware queues' dispatch order (a second kernel on another stream could
   // wait for a CU on its XCD until the persistent grid drains)
   a.heavy_blocks = (int32_t)team_blocks;
+  a.quad_per_wave = ctx->quad_per_wave;
   if (nray > n_heavy || team_blocks) {
     const int64_t grid = team_blocks + (nray > n_heavy ? blocks : 0);
     hipLaunchKernelGGL(rk45_run_kernel<BG>, dim3((unsigned)grid), dim3(256), 0, st, a);
@@ -3725,6 +3736,14 @@ rwrt_status rwrt_ctx_create(int32_t device, rwrt_ctx** out) {
     return s ? s : fail(RWRT_ERR_HIP, "creating the context's stream and events failed%s");
   }
   *out = c;
+  return RWRT_OK;
+}
+
+rwrt_status rwrt_ctx_set_latency_density(rwrt_ctx* c, int32_t rays_per_wave) {
+  if (!c) return fail(RWRT_ERR_ARG, "rwrt_ctx is NULL%s");
+  if (rays_per_wave < 1 || rays_per_wave > 16) return fail(RWRT_ERR_ARG, "rays_per_wave must be 1..16%s");
+  std::lock_guard<std::mutex> lock(c->mu);
+  c->quad_per_wave = rays_per_wave;
   return RWRT_OK;
 }
 

@@ -271,9 +271,11 @@ class RayEngine:
         key = torch.where(frozen, torch.full_like(work, -1), work)
         return torch.sort(key, descending=True, stable=True).indices.to(torch.int64).contiguous()
 
-    # a heavy ray's attempt in rk45_quad_kernel / in a loaded rk45_run_kernel
-    # wave (tools/team_latency.py: 11.5 vs 13.3-13.7 us on the heaviest C3 rays)
-    QUAD_ATTEMPT_RATIO = 0.85
+    # a heavy ray's attempt in latency mode / in a loaded rk45_run_kernel wave
+    # (tools/team_latency.py on the heaviest C3 rays: 10.2 us alone in its
+    # wave, 11.5 us at 16 rays per wave, 13.3-13.7 us in the run kernel)
+    QUAD_RATIO_1 = 0.76
+    QUAD_RATIO_16 = 0.85
     QUAD_MIN_GAIN = 0.07
 
     def team_capacity(self):
@@ -282,44 +284,58 @@ class RayEngine:
 
     def team_size(self, team, st, work, order, rows):
         """How many of the first rays of ``order`` (live at the launch start)
-        go to the latency mode.  An int asks for that many; "auto" picks the
-        number that minimises the launch's predicted makespan from each ray's
-        previous-launch work (below)."""
+        go to the latency mode, and how many of them share a wave: ``(n,
+        rays_per_wave)``.  An int asks for that many (16 per wave), a pair
+        ``(n, rays_per_wave)`` for both; "auto"
+        picks the pair that minimises the launch's predicted makespan from each
+        ray's previous-launch work (below)."""
         if order is None or self.bg is not None:   # (the latency mode is static-background only)
-            return 0
+            return 0, 16
         live = ~torch.isnan(st["state"][:5].sum(0))
         n_live = int(live.sum().item())
-        cap = min(self.team_capacity(), n_live)
-        if team != "auto":
-            n = min(int(team), cap)
-            # the first n entries of the order must be live rays
-            return n if n == 0 or bool(live[order[:n]].all()) else 0
-        if work is None or cap < 1:
-            return 0
-        # predicted makespan of the launch for n heavy rays in latency mode (n a
-        # multiple of its 64 rays per block, each block taking a CU from the
-        # run kernel's persistent grid), in run-kernel attempt times:
-        #   max(heaviest ray x QUAD_ATTEMPT_RATIO,             (latency mode)
-        #       ray n+1, remaining work / remaining lanes)     (run kernel)
-        # and the n that minimises it (the smallest on ties)
-        w = torch.where(live, work, torch.zeros_like(work))[order].to(torch.float64)
         ncu = torch.cuda.get_device_properties(self.device).multi_processor_count
+        if team != "auto":
+            n, q = (int(team[0]), int(team[1])) if isinstance(team, (tuple, list)) else (int(team), 16)
+            n = min(n, (ncu // 2) * 4 * q, n_live)
+            # the first n entries of the order must be live rays
+            return (n if n == 0 or bool(live[order[:n]].all()) else 0), q
+        if work is None or n_live < 1:
+            return 0, 16
+        # predicted makespan for n heavy rays in latency mode at q rays per
+        # wave (4q per block, each block taking a CU from the run kernel's
+        # persistent grid), in run-kernel attempt times:
+        #   max(heaviest ray x QUAD_RATIO(q),                 (latency mode)
+        #       ray n+1, remaining work / remaining lanes)     (run kernel)
+        # minimised over (n, q) (the smallest n, then the densest q, on ties)
+        w = torch.where(live, work, torch.zeros_like(work))[order].to(torch.float64)
         cum = torch.cumsum(w, 0)
-        n = torch.arange(0, cap + 1, 64, device=w.device)
-        n = torch.unique(torch.cat([n, torch.tensor([cap], device=w.device)]))
-        rest = cum[-1] - torch.where(n > 0, cum[(n - 1).clamp(min=0)], torch.zeros_like(cum[:1]))
-        lanes = 256.0 * (ncu - (n + 63) // 64).clamp(min=1)
-        nxt = torch.where(n < w.numel(), w[n.clamp(max=w.numel() - 1)], torch.zeros_like(rest))
-        t = torch.maximum(torch.maximum(nxt, rest / lanes),
-                          torch.where(n > 0, w[0] * self.QUAD_ATTEMPT_RATIO, torch.zeros_like(rest)))
+        best = None
+        for q in (16, 8, 4, 2, 1):
+            cap = min((ncu // 2) * 4 * q, n_live)
+            n = torch.arange(0, cap + 1, 4 * q, device=w.device)
+            n = torch.unique(torch.cat([n, torch.tensor([cap], device=w.device)]))
+            rest = cum[-1] - torch.where(n > 0, cum[(n - 1).clamp(min=0)], torch.zeros_like(cum[:1]))
+            lanes = 256.0 * (ncu - (n + 4 * q - 1) // (4 * q)).clamp(min=1)
+            nxt = torch.where(n < w.numel(), w[n.clamp(max=w.numel() - 1)], torch.zeros_like(rest))
+            ratio = self.QUAD_RATIO_1 + (self.QUAD_RATIO_16 - self.QUAD_RATIO_1) * (q - 1) / 15.0
+            t = torch.maximum(torch.maximum(nxt, rest / lanes),
+                              torch.where(n > 0, w[0] * ratio, torch.zeros_like(rest)))
+            k = int(torch.argmin(t).item())
+            cand = (float(t[k]), int(n[k].item()), q, float(t[0]))
+            if best is None or cand[0] < best[0] - 1e-9 * best[0]:
+                best = cand
+        t_best, n_best, q_best, t_none = best
         # (the prediction ignores what the split costs beyond the CUs: take the
         # latency mode only for a predicted gain of QUAD_MIN_GAIN or more)
-        k = int(torch.argmin(t).item())
-        return int(n[k].item()) if float(t[k]) <= (1.0 - self.QUAD_MIN_GAIN) * float(t[0]) else 0
+        if n_best == 0 or t_best > (1.0 - self.QUAD_MIN_GAIN) * t_none:
+            return 0, 16
+        return n_best, q_best
 
-    def run(self, st, p, tbound, it_begin, it_end, out, order=None, n_heavy=0):
+    def run(self, st, p, tbound, it_begin, it_end, out, order=None, n_heavy=0, rays_per_wave=16):
         """Rows ``[it_begin, it_end)`` into ``out[nray, it_end-it_begin, 8]`` (async)."""
         lib = H.load()
+        if n_heavy:
+            self.ctx.set_latency_density(rays_per_wave)
         if self.bg is None:
             fn, bg = lib.rwrt_rk45_run, H.dptr(self.packed)
         else:
@@ -460,17 +476,17 @@ class RayEngine:
             if order_policy in ("cost", "priority") and prev_work is not None:
                 work = cnt.sum(1) - prev_work
                 order = self.cost_order(st, work)
-            n_heavy = self.team_size(team, st, work, order, i1 - i0) if team else 0
+            n_heavy, qpw = self.team_size(team, st, work, order, i1 - i0) if team else (0, 16)
             if os.environ.get("RWRT_DEBUG_TEAM"):
-                print(f"launch rows [{i0}, {i1}): n_heavy {n_heavy}", flush=True)
+                print(f"launch rows [{i0}, {i1}): n_heavy {n_heavy} at {qpw} per wave", flush=True)
             prev_work = cnt.sum(1)
             if events is not None:
                 e0, e1, es = self._event_pair()
-                self.run(st, p, tb, i0, i1, view, order, n_heavy)
+                self.run(st, p, tb, i0, i1, view, order, n_heavy, qpw)
                 e1.record(es)
                 events.append((e0, e1))
             else:
-                self.run(st, p, tb, i0, i1, view, order, n_heavy)
+                self.run(st, p, tb, i0, i1, view, order, n_heavy, qpw)
             if sink is not None:
                 sink(i0, i1, view)
         mx = int(st["nanrow"].max().item()) if nray else 0

@@ -10,7 +10,7 @@ results bit for bit.
   against the oracle (the reference's arithmetic, NumPy's transcendentals
   included): every value of every row, and the accepted-step counts;
 * C2 (both backgrounds, 10 days, chunked) with every live ray in latency
-  mode against the run kernel alone: rows and per-ray accepted / rejected
+  mode (16, 1 and 4 rays per wave) against the run kernel alone: rows and per-ray accepted / rejected
   counts (reference: wr.py:767-887, rkf45.py:375-514).
 """
 import numpy as np
@@ -70,7 +70,9 @@ def test_team_equals_run_kernel_c2(kind):
         y0 = np.array(initial_rows(bs, lon, lat, cfg.zwn, cfg.freq)[:5]).reshape(5, -1)
     nt = 10 * 12 + 1
     want, rw = rows_of(eng, y0, nt, chunk=40, first_chunk=[7])
-    got, rg = rows_of(eng, y0, nt, chunk=40, first_chunk=[7], team=eng.team_capacity())
-    assert same(got[:, :, :7], want[:, :, :7])
-    assert torch.equal(rg.nacc, rw.nacc) and torch.equal(rg.nrej, rw.nrej)
-    assert torch.equal(rg.nanrow, rw.nanrow)
+    # 16 rays per wave (64 per block), 1 per wave, 4 per wave over a ragged count
+    for team in (eng.team_capacity(), (eng.team_capacity(), 1), (333, 4)):
+        got, rg = rows_of(eng, y0, nt, chunk=40, first_chunk=[7], team=team)
+        assert same(got[:, :, :7], want[:, :, :7]), team
+        assert torch.equal(rg.nacc, rw.nacc) and torch.equal(rg.nrej, rw.nrej), team
+        assert torch.equal(rg.nanrow, rw.nanrow), team
