@@ -277,6 +277,11 @@ class RayEngine:
     QUAD_RATIO_1 = 0.76
     QUAD_RATIO_16 = 0.85
     QUAD_MIN_GAIN = 0.07
+    # rays per wave the auto rule considers: sparser waves measured SLOWER per
+    # heavy ray in a full run (tools/team_latency.py --density, 90 d: 16 / 64
+    # / 256 heaviest rays 0.20 / 0.21 / 0.21 s at 16 per wave, 0.51 / 0.55 /
+    # 0.56 s at 1 per wave, 256 rays 0.27 s at 4 per wave), so only 16
+    QUAD_DENSITIES = (16,)
 
     def team_capacity(self):
         """Rays the latency mode takes at most (64 per CU, half the CUs)."""
@@ -310,7 +315,7 @@ class RayEngine:
         w = torch.where(live, work, torch.zeros_like(work))[order].to(torch.float64)
         cum = torch.cumsum(w, 0)
         best = None
-        for q in (16, 8, 4, 2, 1):
+        for q in self.QUAD_DENSITIES:
             cap = min((ncu // 2) * 4 * q, n_live)
             n = torch.arange(0, cap + 1, 4 * q, device=w.device)
             n = torch.unique(torch.cat([n, torch.tensor([cap], device=w.device)]))

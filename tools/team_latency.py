@@ -43,6 +43,7 @@ def main():
     ap.add_argument("--bg", default="zonal", choices=["zonal", "nonzonal"])
     ap.add_argument("--ks", default="1,64,1024,8192")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--density", type=int, default=16, help="latency mode: rays per wave (1-16)")
     a = ap.parse_args()
     bs, _ = bench.make_bs(a.bg)
     y0 = torch.as_tensor(bench.c3_initial_state(bs), device="cuda")
@@ -51,15 +52,15 @@ def main():
     full = eng.integrate(y0, nt, 7200.0, ttotal=(nt - 1) * 7200.0, first_chunk=[6, 24, 96])
     work = (full.nacc + full.nrej)
     order = torch.sort(work, descending=True, stable=True).indices
-    res = {"days": a.days, "bg": a.bg, "cases": []}
+    res = {"days": a.days, "bg": a.bg, "density": a.density, "cases": []}
     for k in [int(x) for x in a.ks.split(",")]:
-        k = min(k, eng.team_capacity())
+        k = min(k, eng.team_capacity() * a.density // 16)
         idx = order[:k]
         yk = y0[:, idx].contiguous()
         out = torch.empty((k, nt - 1, 8), dtype=torch.float64, device="cuda")
         t_run, r_run = timed(eng, yk, nt, 0, out)
         rows_run = out.clone()
-        t_team, r_team = timed(eng, yk, nt, k, out)
+        t_team, r_team = timed(eng, yk, nt, (k, a.density), out)
         a_, b_ = rows_run[:, :, :7].cpu().numpy(), out[:, :, :7].cpu().numpy()
         same = np.array_equal(np.where(np.isnan(a_), np.nan, a_).view(np.int64),
                               np.where(np.isnan(b_), np.nan, b_).view(np.int64))
