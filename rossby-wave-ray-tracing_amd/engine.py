@@ -276,7 +276,7 @@ class RayEngine:
     # wave, 11.5 us at 16 rays per wave, 13.3-13.7 us in the run kernel)
     QUAD_RATIO_1 = 0.76
     QUAD_RATIO_16 = 0.85
-    QUAD_MIN_GAIN = 0.07
+    QUAD_MIN_GAIN = 0.10   # (one C3 GPU: predicted 6-9 %, measured -1 %)
     # rays per wave the auto rule considers: sparser waves measured SLOWER per
     # heavy ray in a full run (tools/team_latency.py --density, 90 d: 16 / 64
     # / 256 heaviest rays 0.20 / 0.21 / 0.21 s at 16 per wave, 0.51 / 0.55 /
