@@ -2082,6 +2082,47 @@ struct QuadRole {
   }
 };
 
+// lookup_end for a quad: the eleven blends dealt out by record (role r blends
+// records r and r + 4, roles 2 and 3 record r only: u v qxx qxy | ux uy qyy |
+// vx vy | qx qy), 8 LDS reads per lane instead of 24, then broadcast; each
+// field is the same blend of the same corner values (bit for bit).
+#ifndef RWRT_QUAD_BLEND_SPLIT
+#define RWRT_QUAD_BLEND_SPLIT 1
+#endif
+__device__ __forceinline__ void quad_lookup_end(const CachedStaticBG& B, const QuadRole& R,
+                                                const CachedStaticBG::Pending& p, double g[11]) {
+  static_assert(!RWRT_CACHE_LANE_SLICE, "quad_lookup_end reads the chunk-major slice layout");
+  if (p.refilled) lds_dma_wait();
+  Corners k;
+  k.wa = p.wa;
+  k.wb = p.wb;
+  k.wc = p.wc;
+  k.wd = p.wd;
+  const int ra = R.role, rb = R.high ? R.role : R.role + 4;   // (roles 2, 3: a duplicate read)
+  const char* base = B.wave_base + B.lane16;
+  double2 va[4], vb[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    va[j] = *reinterpret_cast<const double2*>(base + (j * 6 + ra) * 1024);
+    vb[j] = *reinterpret_cast<const double2*>(base + (j * 6 + rb) * 1024);
+  }
+  const double ax = blend(k, va[0].x, va[1].x, va[2].x, va[3].x);
+  const double ay = blend(k, va[0].y, va[1].y, va[2].y, va[3].y);
+  const double bx = blend(k, vb[0].x, vb[1].x, vb[2].x, vb[3].x);
+  const double by = blend(k, vb[0].y, vb[1].y, vb[2].y, vb[3].y);
+  g[F_U] = qbcast<0>(ax);
+  g[F_V] = qbcast<0>(ay);
+  g[F_UX] = qbcast<1>(ax);
+  g[F_UY] = qbcast<1>(ay);
+  g[F_VX] = qbcast<2>(ax);
+  g[F_VY] = qbcast<2>(ay);
+  g[F_QX] = qbcast<3>(ax);
+  g[F_QY] = qbcast<3>(ay);
+  g[F_QXX] = qbcast<0>(bx);
+  g[F_QXY] = qbcast<0>(by);
+  g[F_QYY] = qbcast<1>(bx);
+}
+
 // ray_rhs (wr.py:492-556) for one ray per quad: returns dy[role] (rA) and
 // dy[4] (rB); aux as in ray_rhs (every lane).
 __device__ __forceinline__ void quad_rhs(const CachedStaticBG& B, const QuadRole& R, const double* y,
@@ -2096,7 +2137,11 @@ __device__ __forceinline__ void quad_rhs(const CachedStaticBG& B, const QuadRole
   double s, c, tn;
   np_math::nm_sincostan_end(lat, trig, s, c, tn);
   __builtin_amdgcn_sched_barrier(0);
+#if RWRT_QUAD_BLEND_SPLIT
+  quad_lookup_end(B, R, pending, g);
+#else
   lookup_end(B, pending, g);
+#endif
   // Mercator (bs.py:856-883): M.cp == c off the pole band; there every
   // output takes mercator12_masked's extra factor m
   const Merc M = merc_factors(lat, c, s);
