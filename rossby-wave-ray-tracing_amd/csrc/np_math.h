@@ -38,7 +38,12 @@
 
 namespace np_math {
 
-NM_FN double nm_d(unsigned long long u) { return __builtin_bit_cast(double, u); }
+// NM_KVAL(u): an includer may serve the scalar constants from a faster copy
+// (e.g. LDS) when u is a compile-time constant; default: the bit pattern.
+#ifndef NM_KVAL
+#define NM_KVAL(u) __builtin_bit_cast(double, (unsigned long long)(u))
+#endif
+NM_FN double nm_d(unsigned long long u) { return NM_KVAL(u); }
 NM_FN unsigned long long nm_u(double x) { return __builtin_bit_cast(unsigned long long, x); }
 NM_FN double nm_fma(double a, double b, double c) { return __builtin_fma(a, b, c); }
 NM_FN double nm_abs(double x) { return nm_d(nm_u(x) & 0x7FFFFFFFFFFFFFFFull); }

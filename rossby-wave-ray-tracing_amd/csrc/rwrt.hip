@@ -1124,6 +1124,91 @@ __shared__ unsigned long long nm_lds_kP_EXP_LO[16];
 __shared__ unsigned nm_lds_kRCP14_KNOT[128];
 #define NM_LD(t, i) nm_lds_##t[i]
 #endif
+// The NumPy-math polynomial and reduction constants from LDS
+// (RWRT_NM_KLDS): a compile-time constant operand of the math costs one
+// ds_read_b64 issue slot instead of an s_mov_b32 pair rebuilt at each use
+// (SGPR pressure makes the compiler rematerialise them).
+#ifndef RWRT_NM_KLDS
+#define RWRT_NM_KLDS 0
+#endif
+#if RWRT_NM_KLDS && RWRT_NM_LDS && !RWRT_DIAG_NM_TAB0
+#include "np_math_tables.h"
+#define NM_KLIST(X) \
+  X(kG_HP0) \
+  X(kG_HP1) \
+  X(kG_MHP1) \
+  X(kG_T126) \
+  X(kG_S5) \
+  X(kG_S4) \
+  X(kG_S3) \
+  X(kG_S2) \
+  X(kG_S1) \
+  X(kG_BIG) \
+  X(kG_SN5) \
+  X(kG_SN3) \
+  X(kG_CS6) \
+  X(kG_CS4) \
+  X(kG_CS2) \
+  X(kG_TOINT) \
+  X(kG_HPINV) \
+  X(kG_MP1) \
+  X(kG_MP2) \
+  X(kG_PP3) \
+  X(kG_PP4) \
+  X(kT_INVPI16) \
+  X(kT_PI16A) \
+  X(kT_PI16B) \
+  X(kT_PI16C) \
+  X(kT_C1) \
+  X(kT_C2) \
+  X(kT_C3) \
+  X(kT_C4) \
+  X(kT_C5) \
+  X(kT_ONE) \
+  X(kT_SHIFT) \
+  X(kT_BIGARG) \
+  X(kP_HALF) \
+  X(kP_C1) \
+  X(kP_C10) \
+  X(kP_C9) \
+  X(kP_C8) \
+  X(kP_C7) \
+  X(kP_C6) \
+  X(kP_C5) \
+  X(kP_C4) \
+  X(kP_C3) \
+  X(kP_LN) \
+  X(kP_LP) \
+  X(kP_E7) \
+  X(kP_E6) \
+  X(kP_E4) \
+  X(kP_E3) \
+  X(kP_E2) \
+  X(kP_E1) \
+  X(kP_TOVF)
+enum NmKIdx {
+#define NM_KENUM(name) NM_KIDX_##name,
+  NM_KLIST(NM_KENUM)
+#undef NM_KENUM
+  NM_KCOUNT
+};
+__constant__ unsigned long long nm_kvals[NM_KCOUNT] = {
+#define NM_KVALS(name) np_math::name,
+    NM_KLIST(NM_KVALS)
+#undef NM_KVALS
+};
+__shared__ double nm_lds_k[NM_KCOUNT];
+__device__ __forceinline__ double nm_kval(unsigned long long u) {
+  if (__builtin_constant_p(u)) {
+#define NM_KTRY(name) \
+  if (u == np_math::name) return nm_lds_k[NM_KIDX_##name];
+    NM_KLIST(NM_KTRY)
+#undef NM_KTRY
+  }
+  return __builtin_bit_cast(double, u);
+}
+#define NM_KVAL(u) nm_kval(u)
+#endif
 #include "np_math.h"
 
 namespace rwrt {
@@ -1154,6 +1239,9 @@ __device__ __forceinline__ void nm_stage() {
     }
   if (MASK & (NM_TAN | NM_POW))
     for (int i = t; i < 128; i += nt) nm_lds_kRCP14_KNOT[i] = np_math::kRCP14_KNOT[i];
+#if RWRT_NM_KLDS
+  for (int i = t; i < NM_KCOUNT; i += nt) nm_lds_k[i] = __builtin_bit_cast(double, nm_kvals[i]);
+#endif
   __syncthreads();
 #endif
 }
