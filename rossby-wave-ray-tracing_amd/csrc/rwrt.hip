@@ -2373,6 +2373,27 @@ __device__ __forceinline__ double quad_attempt(const CachedStaticBG& B, const Qu
   return sqrt(ss) / RootN<5>::v;
 }
 
+// cal_dis_reaches for a quad (wr.py:844-850): the two half-difference sines
+// on two lanes (role 0: latitude, role 1: longitude), then broadcast
+__device__ __forceinline__ bool quad_dis_reaches(const QuadRole& R, double lon_c, double lat_c,
+                                                 double lon_p, double lat_p, double cos_c,
+                                                 double cos_p, double cut_off, double cut_a) {
+#if RWRT_MATH_NUMPY
+  const double dlat2 = (lat_c - lat_p) / 2.0, dlon2 = (lon_c - lon_p) / 2.0;
+  const double sv = k_sin(R.odd ? dlon2 : dlat2);
+  const double sd = qbcast<0>(sv), sl = qbcast<1>(sv);
+  const double a = sd * sd + (cos_p * cos_c) * (sl * sl);
+  bool r = false;
+  if (!(a < cut_a)) {
+    asm volatile("");   // rare: near or past the threshold, or NaN
+    r = fabs(2.0 * atan2(sqrt(a), sqrt(1.0 - a))) >= cut_off;
+  }
+  return r;
+#else
+  return cal_dis_reaches(lon_c, lat_c, lon_p, lat_p, cos_c, cos_p, cut_off, cut_a);
+#endif
+}
+
 // Rows [it_begin, it_end) of rays order[0, n_heavy), one per quad (64 per
 // block, no queue): rk45_run_kernel's loop, step control and post-processing.
 // Run by rk45_run_kernel's first a.heavy_blocks blocks (one grid: those
@@ -2461,7 +2482,7 @@ __device__ __forceinline__ void quad_rays(const RunArgs<StaticBG>& a, char* cach
     bool masked = fabs(y[1]) >= kHalfPi;
     if (!masked) {
       cos_c = have ? aux[2] : cos_small(y[1]);
-      masked = cal_dis_reaches(y[0], y[1], prev_lon, prev_lat, cos_c, cos_prev, a.cut_off, a.cut_a);
+      masked = quad_dis_reaches(R, y[0], y[1], prev_lon, prev_lat, cos_c, cos_prev, a.cut_off, a.cut_a);
     }
     if (masked) {
 #pragma unroll
