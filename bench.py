@@ -171,6 +171,12 @@ def roofline(steps_per_launch, avg_launch_s, workload, schedule, bytes_per_step,
                    note=("one wave per SIMD (256 VGPR + AGPRs, 146 KB LDS per block): every VALU "
                          "wave-instruction holds its SIMD's issue for >= 4 cycles; peak = 1024 SIMDs x "
                          "in-kernel clock (GRBM_GUI_ACTIVE / 8 / kernel time) / 4"))
+        if "issue_active_frac" in valu:
+            # any instruction type (VALU, SALU, LDS, VMEM, branch) takes the wave's
+            # issue slot at one wave per SIMD: the share of wave cycles that issued
+            out["issue_any"] = {"frac_of_wave_cycles": valu["issue_active_frac"],
+                                "valu_frac_of_wave_cycles": valu.get("valu_active_frac"),
+                                "counters": "SQ_ACTIVE_INST_ANY, SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES"}
     out["hbm"] = {"achieved_GBps": traffic["traffic_bytes_per_launch"] / avg_launch_s / 1e9 if traffic else None,
                   "peak_GBps": HBM_PEAK / 1e9,
                   "frac": traffic["traffic_bytes_per_launch"] / avg_launch_s / HBM_PEAK if traffic else None,
