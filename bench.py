@@ -213,8 +213,9 @@ def main():
     ap.add_argument("--config", default="C3", choices=["C3", "C5"],
                     help="C3 (BASELINE configs[2]/[3], the metric's workload) or C5 (configs[4]: "
                          "0.25-degree time-varying background)")
-    ap.add_argument("--fields", default="fp64", choices=["fp64", "fp32"],
-                    help="C5: storage of the background levels (arithmetic is fp64 either way)")
+    ap.add_argument("--fields", default="fp64", choices=["fp64", "fp32", "fp32a"],
+                    help="C5: storage of the background levels (fp64 arithmetic), or fp32a: fp32 "
+                         "levels and an fp32 RHS (fp64 positions, time and stepper)")
     ap.add_argument("--c5-periods", type=int, default=5,
                     help="C5 periods (1-5 of the C3 list; 5 = 9.67 M slots, ~4 M live rays: BASELINE's size)")
     ap.add_argument("--team", default="auto",
@@ -424,7 +425,8 @@ def main_c5(args, dist, group, rank, world, dev):
     nlev = int(np.ceil((nt - 1) * 7200.0 / dt_bg)) + 1
     b0 = S.background_level(0, res=res)
     t_build = time.perf_counter()
-    lv = Levels(b0["lat"], b0["lon"], nlev, t0=0.0, dt=dt_bg, fp32=(args.fields == "fp32"), device=dev)
+    lv = Levels(b0["lat"], b0["lon"], nlev, t0=0.0, dt=dt_bg, fp32=(args.fields in ("fp32", "fp32a")), device=dev,
+                arith32=(args.fields == "fp32a"))
     for j in range(nlev):
         bj = b0 if j == 0 else S.background_level(j, res=res)
         lv.set_level(j, bj["u"], bj["v"])
@@ -503,7 +505,8 @@ def main_c5(args, dist, group, rank, world, dev):
         print(json.dumps({
             "metric": METRIC, "value": tot_steps / max_el, "unit": "ray-steps/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * max_el / args.steps,
-            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+            "dtype": "f32 RHS, f64 stepper" if args.fields == "fp32a" else "f64",
             "data": "synthetic",
             "config": {"workload": workload, "ray_slots": nslot, "live_rays": n_live,
                        "rows": nt, "levels": nlev, "field_storage": args.fields,

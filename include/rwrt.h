@@ -72,7 +72,8 @@ typedef struct {
 
 /* A time-varying basic state (this framework's extension for BASELINE
  * configs[4]; the reference's fun ignores t, wr.py:784-789): nlev packed
- * levels [nlev][ncol][nrow][12] (fp64, or fp32 when fp32 != 0) valid at
+ * levels [nlev][ncol][nrow][12] (fp64, or fp32 when fp32 != 0; fp32 == 2
+ * also computes the RHS in fp32 -- not the reference's arithmetic) valid at
  * t0 + j*dt seconds of ray time.  The RHS interpolates each level bilinearly
  * exactly like the static state and then linearly in time:
  * s = (t - t0)/dt, j = clip(floor(s), 0, nlev-2), w = clip(s - j, 0, 1),

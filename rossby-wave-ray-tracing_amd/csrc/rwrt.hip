@@ -807,6 +807,13 @@ struct VaryingBG {
   }
 };
 
+// fp32 levels with an fp32 RHS (rwrt_background.fp32 == 2): the fields'
+// blends, the time interpolation, the trigonometry, Mercator, group velocity
+// and tendencies in fp32 (ray_rhs overload below); positions, the cell and
+// level indices, time and the stepper stay fp64.  Not the reference's
+// arithmetic: the fp32-vs-fp64 comparison of BASELINE configs[4].
+struct VaryingBGA32 : VaryingBG<float> {};
+
 // VaryingBG<float> with the same per-lane LDS cache, keyed by (cell, level
 // pair): both bracketing levels' four fp32 corner records (2 x 4 x 48 B = 24
 // chunks of 16 B, the same 24 KiB per wave as the static cache).  A lane
@@ -888,6 +895,35 @@ __device__ __forceinline__ void lookup_end(const CachedVaryingBG32& B,
                                            const CachedVaryingBG32::Pending& p, double g[11]) {
   B.end(p, g);
 }
+
+// VaryingBGA32 through CachedVaryingBG32's cache (the same LDS-DMA refills),
+// blended in fp32 (endf)
+struct CachedVaryingBGA32 : CachedVaryingBG32 {
+  __device__ __forceinline__ void endf(const Pending& p, float g[11]) const {
+    lds_dma_wait();
+    float4 v[2][4][3];
+#pragma unroll
+    for (int lev = 0; lev < 2; ++lev)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) v[lev][j][q] = chunk(lev, j, q);
+    __builtin_amdgcn_sched_barrier(0);
+    const float w0 = (float)p.w[0], w1 = (float)p.w[1], w2 = (float)p.w[2], w3 = (float)p.w[3];
+    const float wt = (float)p.wt;
+#pragma unroll
+    for (int f = 0; f < 11; ++f) {
+      const int q = f >> 2, e = f & 3;
+      auto el = [&](int lev, int j) -> float {
+        const float4& c = v[lev][j][q];
+        return e == 0 ? c.x : e == 1 ? c.y : e == 2 ? c.z : c.w;
+      };
+      const float ga = ((el(0, 0) * w0 + el(0, 1) * w1) + el(0, 2) * w2) + el(0, 3) * w3;
+      const float gb = ((el(1, 0) * w0 + el(1, 1) * w1) + el(1, 2) * w2) + el(1, 3) * w3;
+      g[f] = ga * (1.0f - wt) + gb * wt;
+    }
+  }
+};
 
 // VaryingBG<double> with the per-lane LDS cache holding ONE level: the lower
 // bracketing level's four fp64 corner records (4 x 96 B = the static cache's
@@ -993,6 +1029,21 @@ struct LaneBG<VaryingBG<float>> {
   __device__ static CachedVaryingBG32 make(const VaryingBG<float>& B, char* lds) {
     const unsigned wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     return CachedVaryingBG32{B, lds + wave * kCacheBytesPerWave, (threadIdx.x & 63u) * 16u, ~0u, ~0u, -1};
+  }
+};
+template <>
+struct LaneBG<VaryingBGA32> {
+  using type = CachedVaryingBGA32;
+  static constexpr int kLdsBytes = 4 * kCacheBytesPerWave;
+  __device__ static CachedVaryingBGA32 make(const VaryingBGA32& B, char* lds) {
+    const unsigned wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    CachedVaryingBGA32 c;
+    c.V = B;
+    c.wave_base = lds + wave * kCacheBytesPerWave;
+    c.lane16 = (threadIdx.x & 63u) * 16u;
+    c.key_x = c.key_y = ~0u;
+    c.key_j = -1;
+    return c;
   }
 };
 #ifndef RWRT_CACHE_FP64_LEVELS
@@ -1473,6 +1524,89 @@ __device__ __forceinline__ void ray_rhs(const BG& B, double t, const double* y, 
     aux[1] = vg;
     aux[2] = bad ? kNaN : c;
   }
+}
+
+// ray_rhs with fp32 arithmetic on fp32 levels (VaryingBGA32): the same
+// expressions as ray_rhs / mercator12 / ugvg / core_diffun in float, the
+// device library's sinf/cosf/tanf; dy and aux are returned in fp64.
+// lookup(g) fills the eleven fields (fp32 blends of fp32 levels).
+template <class Lookup>
+__device__ __forceinline__ void ray_rhs_f32(Lookup&& lookup, const double* y, double* dy, double* aux) {
+  const double lat = y[1];
+  const bool bad = fabs(lat) >= kHalfPi || fabs(y[3]) >= 100.0;
+  const float fnan = __builtin_nanf("");
+  const float kx = (float)y[2], ky = bad ? fnan : (float)y[3], amp = (float)y[4];
+  float g[11];
+  lookup(g);
+  if (!(fabs(lat) <= kHalfPi)) {
+#pragma unroll
+    for (int i = 0; i < 11; ++i) g[i] = fnan;
+  }
+  const float latf = (float)lat;
+  float s, c;
+  sincosf(latf, &s, &c);
+  const float tn = tanf(latf);
+  const float m = (fabsf(c) <= 0.0175f) ? 0.0f : 1.0f;
+  const float cp = c * m + (1.0f - m) * 1e-6f;
+  const float fu = g[F_U], fv = g[F_V];
+  const float fmu = (fu / cp) * m, fmv = (fv / cp) * m;
+  const float fmux = (g[F_UX] / cp) * m, fmuy = (g[F_UY] + tn * fu) * m;
+  const float fmvx = (g[F_VX] / cp) * m, fmvy = (g[F_VY] + tn * fv) * m;
+  const float fmqx = g[F_QX] * m, fmqy = (g[F_QY] * cp) * m, fmqxx = g[F_QXX] * m;
+  const float fmqyx = (g[F_QXY] * cp) * m, fmqxy = fmqyx * m;
+  const float fmqyy = (((g[F_QYY] * cp) - (g[F_QY] * s)) * cp) * m;
+  const float kap = ky / kx, kap2 = kap * kap, kap1 = 1.0f + kap2;
+  const float kk = (kx * kx) * kap1, denom = kk * kap1;
+  const float ug = fmu + (((1.0f - kap2) * fmqy) - ((2.0f * kap) * fmqx)) / denom;
+  const float vg = fmv + (((2.0f * kap) * fmqy) + ((1.0f - kap2) * fmqx)) / denom;
+  const float qk = (kap * fmqxx - fmqyx) / kk, ql = (kap * fmqxy - fmqyy) / kk;
+  const float dzwn = (-kx) * ((fmux + kap * fmvx) + qk);
+  const float dmwn = (-kx) * ((fmuy + kap * fmvy) + ql);
+  const float damp1 = (2.0f * ((fmux + fmvy) + kap * (fmvx + fmuy))) / kap1;
+  const float damp2 = (2.0f * (kap * (fmqxx - fmqyy) + (kap2 - 1.0f) * fmqxy)) / denom;
+  const float damp = (damp1 + damp2) + (-2.0f * s) * fmv;
+  const float rinv = (float)(1.0 / kREarth);
+  dy[0] = (double)(ug * rinv);
+  dy[1] = (double)((vg * c) * rinv);
+  dy[2] = (double)(dzwn * rinv);
+  dy[3] = (double)(dmwn * rinv);
+  dy[4] = (double)((damp * amp) * rinv);
+  if (aux) {
+    aux[0] = ug;
+    aux[1] = vg;
+    aux[2] = bad ? kNaN : (double)c;
+  }
+}
+// plain gathers (rwrt_rhs_tv, the initial step)
+__device__ __forceinline__ void ray_rhs(const VaryingBGA32& B, double t, const double* y, double* dy,
+                                        double* aux = nullptr) {
+  ray_rhs_f32(
+      [&](float g[11]) {
+        unsigned o[4];
+        double wd[4], wtd;
+        B.cell(y[0], y[1], o, wd);
+        const float* A = B.level(t, wtd);
+        const float* L1 = A + (B.nlev > 1 ? B.lev_stride : 0);
+        const float w0 = (float)wd[0], w1 = (float)wd[1], w2 = (float)wd[2], w3 = (float)wd[3];
+        const float wt = (float)wtd;
+#pragma unroll
+        for (int q = 0; q < 11; ++q) {
+          const float ga = ((A[o[0] + q] * w0 + A[o[1] + q] * w1) + A[o[2] + q] * w2) + A[o[3] + q] * w3;
+          const float gb = ((L1[o[0] + q] * w0 + L1[o[1] + q] * w1) + L1[o[2] + q] * w2) + L1[o[3] + q] * w3;
+          g[q] = ga * (1.0f - wt) + gb * wt;
+        }
+      },
+      y, dy, aux);
+}
+// through the ray loop's per-lane LDS cache (rk45_run_kernel)
+__device__ __forceinline__ void ray_rhs(const CachedVaryingBGA32& B, double t, const double* y, double* dy,
+                                        double* aux = nullptr) {
+  ray_rhs_f32(
+      [&](float g[11]) {
+        const auto p = B.begin(y[0], y[1], t);
+        B.endf(p, g);
+      },
+      y, dy, aux);
 }
 
 // group velocity at a stored position (wr.py:856-865): no |l| mask here
@@ -3530,7 +3664,7 @@ rwrt_status launch_init(const BG& B, int64_t nray, const double* d_y0, const rwr
 struct rwrt_ctx {
   int device = 0;
   int ncu = 256;
-  int blocks_static = 0, blocks_f32 = 0, blocks_f64 = 0;   // persistent grids
+  int blocks_static = 0, blocks_f32 = 0, blocks_f64 = 0, blocks_a32 = 0;   // persistent grids
   uint8_t* flags = nullptr;
   size_t cap = 0;
   hipStream_t side = nullptr;
@@ -3579,6 +3713,7 @@ template <class BG> int& ctx_blocks(rwrt_ctx* c);
 template <> int& ctx_blocks<StaticBG>(rwrt_ctx* c) { return c->blocks_static; }
 template <> int& ctx_blocks<VaryingBG<float>>(rwrt_ctx* c) { return c->blocks_f32; }
 template <> int& ctx_blocks<VaryingBG<double>>(rwrt_ctx* c) { return c->blocks_f64; }
+template <> int& ctx_blocks<VaryingBGA32>(rwrt_ctx* c) { return c->blocks_a32; }
 
 template <class BG>
 int ctx_persistent_blocks(rwrt_ctx* c) {
@@ -4013,6 +4148,11 @@ rwrt_status rwrt_rk45_init_tv(const rwrt_grid* g, const rwrt_background* b, int6
                               const double* d_y0, const rwrt_params* p, double* d_state,
                               int64_t* d_count, int32_t* d_nanrow, int32_t* d_live,
                               int64_t* d_summary, void* stream) {
+  if (b && b->fp32 == 2) {
+    VaryingBGA32 B;
+    if (rwrt_status s = make_varying(g, b, static_cast<VaryingBG<float>&>(B))) return s;
+    return launch_init(B, nray, d_y0, p, d_state, d_count, d_nanrow, d_live, d_summary, stream);
+  }
   if (b && b->fp32) {
     VaryingBG<float> B;
     if (rwrt_status s = make_varying(g, b, B)) return s;
@@ -4028,6 +4168,12 @@ rwrt_status rwrt_rk45_run_tv(rwrt_ctx* ctx, const rwrt_grid* g, const rwrt_backg
                              int32_t it_end, const int64_t* d_order, int64_t n_heavy,
                              double* d_state, int64_t* d_count, int32_t* d_nanrow, double* d_out,
                              int32_t* d_work, void* stream) {
+  if (b && b->fp32 == 2) {
+    VaryingBGA32 B;
+    if (rwrt_status s = make_varying(g, b, static_cast<VaryingBG<float>&>(B))) return s;
+    return launch_run(ctx, B, nray, p, d_tbound, it_begin, it_end, d_order, n_heavy, d_state, d_count,
+                      d_nanrow, d_out, d_work, stream);
+  }
   if (b && b->fp32) {
     VaryingBG<float> B;
     if (rwrt_status s = make_varying(g, b, B)) return s;
@@ -4045,7 +4191,12 @@ rwrt_status rwrt_rhs_tv(const rwrt_grid* g, const rwrt_background* b, int64_t n,
   if (n < 0 || !d_t || !d_y || !d_dydt) return fail(RWRT_ERR_ARG, "bad rwrt_rhs_tv arguments%s");
   if (n == 0) return RWRT_OK;
   const dim3 grid(grid_for(n, 256)), block(256);
-  if (b && b->fp32) {
+  if (b && b->fp32 == 2) {
+    VaryingBGA32 B;
+    if (rwrt_status s = make_varying(g, b, static_cast<VaryingBG<float>&>(B))) return s;
+    hipLaunchKernelGGL(rhs_bg_kernel<VaryingBGA32>, grid, block, 0, (hipStream_t)stream, B, n,
+                       d_t, d_y, d_dydt);
+  } else if (b && b->fp32) {
     VaryingBG<float> B;
     if (rwrt_status s = make_varying(g, b, B)) return s;
     hipLaunchKernelGGL(rhs_bg_kernel<VaryingBG<float>>, grid, block, 0, (hipStream_t)stream, B, n,

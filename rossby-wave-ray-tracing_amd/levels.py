@@ -35,9 +35,15 @@ def trig_table(lat):
 class Levels:
     """``nlev`` basic states on one GPU, packed for the ray kernels."""
 
-    def __init__(self, lat_deg, lon_deg, nlev, t0=0.0, dt=6 * 3600.0, fp32=False, device=None):
+    def __init__(self, lat_deg, lon_deg, nlev, t0=0.0, dt=6 * 3600.0, fp32=False, device=None,
+                 arith32=False):
         """Axes in degrees (float32, as read from a file); level ``j`` is valid
-        at ``t0 + j*dt`` s of ray time (the initial rays use level 0: t0 = 0)."""
+        at ``t0 + j*dt`` s of ray time (the initial rays use level 0: t0 = 0).
+        ``arith32`` (fp32 levels only): the RHS computes in fp32 as well
+        (rwrt_background.fp32 = 2; not the reference's arithmetic)."""
+        if arith32 and not fp32:
+            raise ValueError("arith32 needs fp32 levels")
+        self.arith32 = bool(arith32)
         H.require_gpu()
         H.load()
         lat_deg = np.asarray(lat_deg, np.float32)
@@ -85,4 +91,5 @@ class Levels:
 
     def background(self):
         """The ``rwrt_background`` description of these levels."""
-        return H.Background(self.packed.data_ptr(), self.nlev, int(self.fp32), self.t0, self.dt)
+        return H.Background(self.packed.data_ptr(), self.nlev, 2 if self.arith32 else int(self.fp32),
+                            self.t0, self.dt)

@@ -147,3 +147,56 @@ def test_tv_trajectories_vs_oracle(fp32):
                 (np.percentile(dug, 99), dug.max(), d.max())
     n_gpu = int(res.nacc.sum().item())
     assert abs(n_gpu - int(nacc.sum())) <= 0.01 * int(nacc.sum())
+
+
+def test_fp32_arithmetic_tracks_fp64():
+    """rwrt_background.fp32 = 2 (BASELINE configs[4]'s fp32-vs-fp64): fp32
+    levels and an fp32 RHS, fp64 stepper.  Not the reference's arithmetic, so
+    the check is against the fp64-arithmetic run on the same fp32 levels: the
+    RHS to fp32 precision (1e-4 of each component's scale), the C2 rays'
+    2-h positions (99 % within 1e-4 rad) and the same live rays."""
+    from engine import RayEngine
+    from levels import Levels
+    eng64, _, _ = tv(True)
+    nlev = 5
+    bl = [S.background_level(j) for j in range(nlev)]
+    lv = Levels(bl[0]["lat"], bl[0]["lon"], nlev, t0=0.0, dt=DT, fp32=True, arith32=True)
+    for j, b in enumerate(bl):
+        lv.set_level(j, b["u"], b["v"])
+    eng32 = RayEngine.from_levels(lv)
+    rng = np.random.default_rng(5)
+    n = 4096
+    y = np.empty((5, n))
+    y[0] = rng.uniform(-1.0, 8.0, n)
+    y[1] = rng.uniform(-1.4, 1.4, n)
+    y[2] = rng.integers(1, 8, n).astype(float) / 6.371e6
+    y[3] = rng.uniform(-8, 8, n) / 6.371e6
+    y[4] = rng.uniform(0.5, 2.0, n)
+    t = rng.uniform(0.0, 4 * DT, n)
+    a = eng32.rhs_t(t, y).cpu().numpy()
+    b = eng64.rhs_t(t, y).cpu().numpy()
+    assert np.array_equal(np.isnan(a), np.isnan(b))
+    for v in range(5):
+        ok = ~np.isnan(b[v])
+        scale = np.max(np.abs(b[v][ok]))
+        assert np.max(np.abs(a[v][ok] - b[v][ok])) <= 1e-4 * scale, v
+    cfg = S.config("C2")
+    slon, slat = O.source_matrix(cfg.SW_lon, cfg.SW_lat, cfg.dlon, cfg.dlat, cfg.nnx, cfg.nny)
+    y0 = eng64.initial_rows(slon, slat, cfg.zwn, cfg.freq)[:5].reshape(5, -1)
+    nt = 2
+
+    def first_row(eng):
+        got = {}
+        eng.integrate(y0.clone(), nt, 7200.0, ttotal=7200.0,
+                      sink=lambda i0, i1, o: got.__setitem__(i0, o.cpu().numpy().copy()))
+        return got[1][:, 0, :2]
+    p32, p64 = first_row(eng32), first_row(eng64)
+    assert np.array_equal(np.isnan(p32[:, 0]), np.isnan(p64[:, 0]))
+    ok = ~np.isnan(p64).any(1)
+    assert ok.sum() > 100
+    d = np.max(np.abs(p32[ok] - p64[ok]), axis=1)
+    # the group velocity is a difference of comparable terms (U against the
+    # beta / k^2 terms of a near-stationary wave): fp32's 6e-8 grows to 1e-5-
+    # 1e-4 relative there, 2e-5 rad at the 99th percentile after 2 h
+    # (measured; most rays agree to 1e-9)
+    assert np.percentile(d, 99) <= 1e-4 and d.max() <= 1e-3, (np.percentile(d, 99), d.max())
