@@ -210,7 +210,8 @@ def main():
                     help="rows of the probe launch over every ray whose attempts split and order the set")
     ap.add_argument("--first-chunk", default=None,
                     help="rows of the short launches after the probe that re-measure per-ray cost "
-                         "(default C3 24,160 -- profiles/r2/ab/launch_sweep.txt --, C5 24,96)")
+                         "(default: C3 on one GPU 24,160 -- profiles/r2/ab/launch_sweep.txt --, "
+                         "otherwise 24,96)")
     ap.add_argument("--config", default="C3", choices=["C3", "C5"],
                     help="C3 (BASELINE configs[2]/[3], the metric's workload) or C5 (configs[4]: "
                          "0.25-degree time-varying background)")
@@ -229,7 +230,10 @@ def main():
                     help="diagnostic: repeat the ray batch k times (more rays per lane)")
     args = ap.parse_args()
     if args.first_chunk is None:
-        args.first_chunk = "24,160" if args.config == "C3" else "24,96"
+        # one GPU (throughput-bound): a longer second re-ordering launch orders
+        # the last one better; a split set (heavy-ray-bound) and C5: 24 + 96
+        one = int(os.environ.get("WORLD_SIZE", "1")) == 1
+        args.first_chunk = "24,160" if (args.config == "C3" and one) else "24,96"
     if args.lib:
         os.environ["RWRT_LIB"] = os.path.abspath(args.lib)
 

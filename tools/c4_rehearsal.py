@@ -45,7 +45,7 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--bg", default="zonal", choices=["zonal", "nonzonal"])
     ap.add_argument("--team", default="auto", help="latency-mode rays per launch (int or 'auto')")
-    ap.add_argument("--lead", default="24,96", help="rows of the re-ordering launches after the probe")
+    ap.add_argument("--lead", default="24,96", help="rows of the re-ordering launches after the probe (bench.py default for N > 1)")
     a = ap.parse_args()
     team = a.team if a.team == "auto" else int(a.team)
     lead = [int(x) for x in a.lead.split(",") if x]
