@@ -221,7 +221,7 @@ def main():
     ap.add_argument("--c5-periods", type=int, default=5,
                     help="C5 periods (1-5 of the C3 list; 5 = 9.67 M slots, ~4 M live rays: BASELINE's size)")
     ap.add_argument("--team", default="auto",
-                    help="rays per launch in latency mode (rk45_quad_kernel: four lanes per ray); "
+                    help="rays per launch in latency mode (quad_rays: four lanes of a wave per ray); "
                          "an integer or 'auto' (RayEngine.team_size)")
     ap.add_argument("--lib", default=None, help="alternative librwrt build (A/B timing)")
     ap.add_argument("--traffic", default=None, help="traffic.json (tools/pmc_traffic.py)")
@@ -352,8 +352,8 @@ def main():
                        "rows_per_launch": chunk, "launch_rows": schedule,
                        "rank0_rays": n_mine,
                        "latency_mode": (f"rays above 1.5x the per-lane share of a launch's work run "
-                                        f"in rk45_quad_kernel (four lanes per ray)" if args.team == "auto"
-                                        else f"{args.team} rays per launch in rk45_quad_kernel"),
+                                        f"in latency mode (quad_rays: four lanes per ray)" if args.team == "auto"
+                                        else f"{args.team} rays per launch in latency mode (quad_rays)"),
                        "parallelism": (f"one ray set over {world} GPU(s): cost-balanced split by a "
                                        f"{args.probe}-row probe, RCCL broadcast of the basic state and "
                                        f"gather of endpoints + step counters inside the timed step")},

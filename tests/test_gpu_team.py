@@ -1,4 +1,4 @@
-"""Latency mode: rk45_quad_kernel (csrc/rwrt.hip; four lanes of a wave per
+"""Latency mode: quad_rays (csrc/rwrt.hip, in rk45_run_kernel's first blocks; four lanes of a wave per
 ray, the RHS's divisions, stage sums and error norm dealt out over the quad
 and exchanged by DPP) -- or, in a RWRT_LATENCY_QUAD=0 build, rk45_team_kernel
 (each RHS split over the four waves of a block) -- must give the run kernel's
