@@ -351,8 +351,9 @@ def main():
                        "ray_slots": nslot, "live_rays": n_live, "rows": nt,
                        "rows_per_launch": chunk, "launch_rows": schedule,
                        "rank0_rays": n_mine,
-                       "latency_mode": (f"rays above 1.5x the per-lane share of a launch's work run "
-                                        f"in latency mode (quad_rays: four lanes per ray)" if args.team == "auto"
+                       "latency_mode": ("per launch, the heaviest rays whose move to quad_rays (four lanes of a "
+                                        "wave per ray) minimises the predicted makespan by >= 10 %"
+                                        if args.team == "auto"
                                         else f"{args.team} rays per launch in latency mode (quad_rays)"),
                        "parallelism": (f"one ray set over {world} GPU(s): cost-balanced split by a "
                                        f"{args.probe}-row probe, RCCL broadcast of the basic state and "
