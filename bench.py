@@ -46,8 +46,9 @@ BYTES_PER_STEP = 2112          # 6 RHS evals x 4 corners x 11 fields x 8 B (SURV
 HBM_PEAK = 8.0e12              # MI355X_MICROARCH.md, chip-level parameters
 
 
-def c3_initial_state(bs, lon_offset_deg=0.0, periods=S.C3_PERIODS_DAYS):
-    """Initial ray state y0[5, nslot] of C3 (all periods concatenated)."""
+def c3_rows(bs, lon_offset_deg=0.0, periods=S.C3_PERIODS_DAYS):
+    """The 7 initial rows (lon lat k l amp ug vg; ``WR.ray_initial_numpy``,
+    host) of every C3 slot, all periods concatenated: ``[7, nslot]``."""
     from wr import initial_rows
     cfg = S.config("C3")
     deg2rad = np.pi / 180.0
@@ -58,8 +59,13 @@ def c3_initial_state(bs, lon_offset_deg=0.0, periods=S.C3_PERIODS_DAYS):
     for P in periods:
         with np.errstate(all="ignore"):
             rows = initial_rows(bs, lon, lat, cfg.zwn, S.c3_freq(P))
-        ys.append(np.array(rows[:5]).reshape(5, -1))
+        ys.append(np.array(rows).reshape(7, -1))
     return np.concatenate(ys, axis=1)
+
+
+def c3_initial_state(bs, lon_offset_deg=0.0, periods=S.C3_PERIODS_DAYS):
+    """Initial ray state y0[5, nslot] of C3 (all periods concatenated)."""
+    return np.ascontiguousarray(c3_rows(bs, lon_offset_deg, periods)[:5])
 
 
 def c3_sources(eng, lon_offset_deg=0.0, periods=S.C3_PERIODS_DAYS):
@@ -125,6 +131,16 @@ def library_sha():
     return hashlib.sha256(open(H.LIB_PATH, "rb").read()).hexdigest()[:16]
 
 
+def endpoint_sha(ends):
+    """sha256 (16 hex digits) of a ray set's last rows (NaN canonicalised):
+    rank 0's set is the same at every N (weak scaling), so its endpoints must
+    hash the same in the 1-GPU and the N-GPU lines."""
+    import hashlib
+    e = ends.detach().cpu().numpy().astype(np.float64, copy=True)
+    e[np.isnan(e)] = np.nan
+    return hashlib.sha256(np.ascontiguousarray(e).tobytes()).hexdigest()[:16]
+
+
 def find_profile(name, path, workload, schedule):
     """A per-launch profile summary (profiles/<round>/.../<name>) of this
     workload run with the same launch schedule (rows per launch), taken on
@@ -188,9 +204,79 @@ def roofline(steps_per_launch, avg_launch_s, workload, schedule, bytes_per_step,
     return out
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def resolve_world(gpus, env=None):
+    """How this process takes part in an N-GPU run: ``("spawn", N)`` -- no
+    launcher set WORLD_SIZE and N > 1, so this process starts the N ranks
+    itself -- or ``("rank", world)`` -- run as one rank (N = 1, or under
+    torch.distributed.run).  ``--gpus`` that disagrees with a launcher's
+    WORLD_SIZE is an error, never silently ignored."""
+    env = os.environ if env is None else env
+    if "WORLD_SIZE" in env:
+        world = int(env["WORLD_SIZE"])
+        if gpus is not None and gpus != world:
+            raise SystemExit(f"bench.py: --gpus {gpus} but the launcher started WORLD_SIZE={world} ranks")
+        return "rank", world
+    n = 1 if gpus is None else int(gpus)
+    if n < 1:
+        raise SystemExit(f"bench.py: --gpus must be >= 1 (got {n})")
+    return ("spawn", n) if n > 1 else ("rank", 1)
+
+
+def spawn_ranks(n, argv, timeout=None):
+    """Start ``n`` ranks of this script (one per GPU, local rank r -> GPU r),
+    rendezvous on 127.0.0.1; rank 0 prints the JSON line.  The parent never
+    touches the GPU (it only starts children and waits), and a rank that fails
+    takes the others down with it.  Returns the worst exit code."""
+    import signal
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    t0 = time.time()
+    rc = 0
+    while any(p.poll() is None for p in procs):
+        bad = [p.returncode for p in procs if p.returncode not in (None, 0)]
+        late = timeout is not None and time.time() - t0 > timeout
+        if bad or late:
+            rc = bad[0] if bad else 124
+            for p in procs:
+                if p.poll() is None:
+                    p.send_signal(signal.SIGTERM)
+            for p in procs:
+                try:
+                    p.wait(timeout=30)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+            break
+        time.sleep(0.2)
+    for p in procs:
+        rc = rc or (p.returncode or 0)
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (one rank each); without a launcher, N > 1 starts the N ranks itself")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="weak: every rank integrates its own full C3 set (the seed grid shifted by "
+                         "rank x 2/N degrees of longitude: N GPUs trace an N-times denser seed grid); "
+                         "strong: ONE C3 set split over the ranks by measured cost (shard.run_sharded)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="set up the ranks and the process group, print the line's skeleton, stop "
+                         "(tests the launcher without a GPU)")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--days", type=float, default=90.0, help="integration horizon per step")
@@ -229,47 +315,73 @@ def main():
     ap.add_argument("--replicate", type=int, default=1,
                     help="diagnostic: repeat the ray batch k times (more rays per lane)")
     args = ap.parse_args()
+    how, world = resolve_world(args.gpus)
+    if how == "spawn":
+        # no launcher: start the N ranks here, before anything touches the GPU
+        return spawn_ranks(world, sys.argv[1:])
     if args.first_chunk is None:
-        # one GPU (throughput-bound): a longer second re-ordering launch orders
-        # the last one better; a split set (heavy-ray-bound) and C5: 24 + 96
-        one = int(os.environ.get("WORLD_SIZE", "1")) == 1
-        args.first_chunk = "24,160" if (args.config == "C3" and one) else "24,96"
+        # a whole set on one GPU (throughput-bound): a longer second
+        # re-ordering launch orders the last one better; a split set
+        # (heavy-ray-bound) and C5: 24 + 96
+        whole = world == 1 or args.scaling == "weak"
+        args.first_chunk = "24,160" if (args.config == "C3" and whole) else "24,96"
     if args.lib:
         os.environ["RWRT_LIB"] = os.path.abspath(args.lib)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = group = None
+    backend = None
+    share = 1                                    # ranks sharing this rank's GPU
     if world > 1:
         import torch.distributed as dist
-        # one GPU per rank; RWRT_DIST_BACKEND=gloo with fewer GPUs than ranks
-        # is the single-GPU rehearsal of this path (ranks share a device)
-        local = local % max(torch.cuda.device_count(), 1)
-        torch.cuda.set_device(local)
-        dist.init_process_group(os.environ.get("RWRT_DIST_BACKEND", "nccl"))
+        # one GPU per rank over RCCL ("nccl"); with fewer GPUs than ranks (the
+        # one-GPU rehearsal) ranks share a device and talk over gloo
+        ndev = torch.cuda.device_count()
+        share = max(1, -(-world // max(ndev, 1)))
+        backend = os.environ.get("RWRT_DIST_BACKEND") or ("nccl" if ndev >= world else "gloo")
+        if ndev:
+            local = local % ndev
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend, rank=rank, world_size=world)
         group = dist.group.WORLD
+    if args.dry_run:
+        if dist:
+            t = torch.ones(1)
+            if backend == "gloo":
+                dist.all_reduce(t)
+            dist.barrier()
+        if rank == 0:
+            print(json.dumps({"metric": METRIC, "value": None, "n_gpus": world, "dry_run": True,
+                              "backend": backend, "scaling": args.scaling,
+                              "world_sum": float(t.item()) if dist else 1.0}), flush=True)
+        if dist:
+            dist.destroy_process_group()
+        return 0
     dev = torch.device("cuda", local if world > 1 else 0)
 
     if args.config == "C5":
-        return main_c5(args, dist, group, rank, world, dev)
+        return main_c5(args, dist, group, rank, world, dev, share)
     from engine import RayEngine
     from shard import run_sharded
+    weak = args.scaling == "weak"
     bs, bg = make_bs(args.bg)
     periods = S.C3_PERIODS_DAYS[: args.periods]
+    # weak scaling: rank r traces the C3 seed grid shifted by r x dlon / N
+    # degrees of longitude (N GPUs: an N-times denser grid; rank 0 = C3)
+    offset = rank * S.config("C3").dlon / world if weak else 0.0
     t_init = time.perf_counter()
-    y0 = c3_initial_state(bs, periods=periods)
+    y0 = c3_initial_state(bs, offset, periods=periods) if (rank == 0 or args.replicate > 1) else None
     t_init = time.perf_counter() - t_init
     if args.replicate > 1:
         y0 = np.concatenate([y0] * args.replicate, axis=1)
-    nslot = y0.shape[1]
-    n_live = int(np.sum(~np.isnan(y0.mean(axis=0))))
     eng = RayEngine.from_bs(bs, device=dev)
     nt = int(round(args.days * 12)) + 1
     gpu_init = args.replicate == 1
+    init_same = None
     if gpu_init:
         # sources and per-k constants resident in HBM; the step starts from them
-        src, zcs = c3_sources(eng, 0.0, periods)
+        src, zcs = c3_sources(eng, offset, periods)
         init_rows = [None] * len(zcs)
         init_info = torch.zeros(1, dtype=torch.int32, device=dev)
 
@@ -280,28 +392,59 @@ def main():
                 ys.append(init_rows[j][:5].reshape(5, -1))
             return torch.cat(ys, dim=1)
         y0_d = make_y0()
-        hy = torch.as_tensor(y0)
-        init_same = bool(((y0_d.cpu() == hy) | (torch.isnan(y0_d.cpu()) & torch.isnan(hy))).all())
+        if y0 is not None:
+            hy = torch.as_tensor(y0)
+            init_same = bool(((y0_d.cpu() == hy) | (torch.isnan(y0_d.cpu()) & torch.isnan(hy))).all())
     else:
-        init_same = None
         y0_d = torch.as_tensor(y0, device=dev)
+    nslot = y0_d.shape[1]
+    live_idx = torch.nonzero(~torch.isnan(y0_d.sum(0))).squeeze(1)
+    n_live = int(live_idx.numel())
     # this rank's rows stay in HBM (C3 on one GPU: 166 GB of 288 GB), so the
     # ray loop is a few launches: the probe, two short re-ordering launches,
-    # then all the rest
-    n_local = -(-nslot // world) + 2                 # shard size bound (cost_partition)
-    free = torch.cuda.mem_get_info(dev)[0]
+    # then all the rest (ranks sharing a GPU share its memory)
+    n_local = nslot if weak else -(-nslot // world) + 2       # shard size bound (cost_partition)
+    free = torch.cuda.mem_get_info(dev)[0] // share
     chunk = args.chunk or max(1, min(nt - 1, int(0.8 * free) // (n_local * 64)))
     out = torch.empty((n_local, min(chunk, nt - 1), 8), dtype=torch.float64, device=dev)
     lead = [int(x) for x in str(args.first_chunk).split(",") if x]
+    team = args.team if args.team == "auto" else int(args.team)
+    gather_dev = torch.device("cpu") if backend == "gloo" else dev
+    n_live_max = n_live
+    if weak and dist:
+        t = torch.tensor([n_live], dtype=torch.int64, device=gather_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+        n_live_max = int(t.item())
+    gathered = {}
+
+    def gather_endpoints(r):
+        """Weak scaling: every rank's live rays' last rows (lon lat k l amp ug
+        vg nacc) gathered to rank 0 (RCCL gather over xGMI)."""
+        ends = r.endpoints[live_idx]
+        if not dist:
+            gathered["rank0"] = ends
+            return
+        pad = torch.full((n_live_max, 8), float("nan"), dtype=torch.float64, device=gather_dev)
+        pad[:n_live] = ends.to(gather_dev)
+        bufs = [torch.empty_like(pad) for _ in range(world)] if rank == 0 else None
+        dist.gather(pad, bufs, dst=0, group=group)
+        if rank == 0:
+            gathered["rank0"] = bufs[0][:n_live]
+            gathered["all"] = bufs
 
     def one_step(events=None):
         if dist is not None:
             dist.broadcast(eng.packed, 0, group=group)   # rank 0's basic state (RCCL over xGMI)
         y = make_y0() if gpu_init else y0_d
+        if weak:
+            r = run_sharded(eng, y, nt, 7200.0, rank=0, world=1, probe=args.probe, lead=lead,
+                            chunk=chunk, out=out, events=events, ttotal=(nt - 1) * 7200.0,
+                            order_policy=args.order, team=team)
+            gather_endpoints(r)
+            return r
         return run_sharded(eng, y, nt, 7200.0, group=group, probe=args.probe, lead=lead,
                            chunk=chunk, out=out, events=events, ttotal=(nt - 1) * 7200.0,
-                           order_policy=args.order,
-                           team=args.team if args.team == "auto" else int(args.team))
+                           order_policy=args.order, team=team)
 
     for _ in range(args.warmup):
         one_step()
@@ -325,7 +468,7 @@ def main():
 
     tot_steps, max_el, tot_rej = steps_done, elapsed, rej
     if dist:
-        t = torch.tensor([float(steps_done), elapsed, float(rej)], dtype=torch.float64, device=dev)
+        t = torch.tensor([float(steps_done), elapsed, float(rej)], dtype=torch.float64, device=gather_dev)
         s = t.clone()
         dist.all_reduce(s, op=dist.ReduceOp.SUM)
         m = t.clone()
@@ -340,35 +483,51 @@ def main():
         workload = (f"C3: 2deg global seeds x k=1..10 x {args.periods} periods, "
                     f"{args.days:g} d at 2 h, 2.5deg DJF jet background"
                     + (" (non-zonal variant)" if args.bg == "nonzonal" else "")
-                    + (" (BASELINE configs[2])" if world == 1 else " (BASELINE configs[3]: C4)"))
+                    + (" (BASELINE configs[2])" if world == 1 else
+                       (" per GPU, the seed grid shifted by rank x 2/N deg of longitude (BASELINE configs[3], "
+                        "weak scaling)" if weak else " (BASELINE configs[3]: C4, one set split)")))
         schedule = [args.probe] + [b - a for a, b in r.res.bounds]
+        if weak:
+            par = (f"{world} rank(s), one GPU each (backend {backend or 'none'}): each integrates its own "
+                   f"C3 seed grid (2.40 M slots), no exchange during integration; inside the timed step "
+                   f"rank 0's basic state is broadcast (RCCL) and every rank's live-ray endpoints + "
+                   f"accepted-step counts are gathered to rank 0 (RCCL gather)")
+        else:
+            par = (f"one ray set over {world} GPU(s): cost-balanced split by a "
+                   f"{args.probe}-row probe, RCCL broadcast of the basic state and "
+                   f"gather of endpoints + step counters inside the timed step")
+        ends0 = gathered.get("rank0") if weak else r.endpoints[live_idx.to(r.endpoints.device)]
         result = {
             "metric": METRIC, "value": value, "unit": "ray-steps/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": 1e3 * max_el / args.steps, "higher_is_better": True,
-            "scaling": "strong", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "scaling": "weak" if weak else "strong", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
             "config": {"workload": workload,
-                       "ray_slots": nslot, "live_rays": n_live, "rows": nt,
-                       "rows_per_launch": chunk, "launch_rows": schedule,
+                       "ray_slots": nslot * (world if weak else 1), "live_rays_rank0": n_live,
+                       "rows": nt, "rows_per_launch": chunk, "launch_rows": schedule,
                        "rank0_rays": n_mine,
                        "latency_mode": ("per launch, the heaviest rays whose move to quad_rays (four lanes of a "
                                         "wave per ray) minimises the predicted makespan by >= 10 %"
                                         if args.team == "auto"
                                         else f"{args.team} rays per launch in latency mode (quad_rays)"),
-                       "parallelism": (f"one ray set over {world} GPU(s): cost-balanced split by a "
-                                       f"{args.probe}-row probe, RCCL broadcast of the basic state and "
-                                       f"gather of endpoints + step counters inside the timed step")},
+                       "parallelism": par},
             "ray_steps_per_step": tot_steps / args.steps,
+            "ray_steps_per_step_rank0": steps_done / args.steps,
             "rejected_per_accepted": tot_rej * args.steps / max(tot_steps, 1),
             "host_init_s": t_init,
             "init": ("GPU rwrt_ray_initial inside every timed step (bit-identical to the host rows)"
                      if gpu_init else "host NumPy rows, outside the timed region"),
             "init_bitwise_vs_host": init_same,
+            "endpoints_rank0_sha256": endpoint_sha(ends0) if ends0 is not None else None,
             "queue_order": args.order,
             "library": os.path.basename(os.environ.get("RWRT_LIB", "librwrt.so")),
             "library_sha256": library_sha(),
             "roofline": roofline(per_launch_steps, avg_launch_s, workload, schedule, BYTES_PER_STEP, args),
         }
+        if weak and "all" in gathered:
+            result["gathered_endpoints"] = {
+                "rows_per_rank": n_live_max, "bytes": world * n_live_max * 64,
+                "alive_at_end": int(sum(int((~torch.isnan(b[:, 0])).sum().item()) for b in gathered["all"]))}
         if world == 1 and not args.no_cpu:
             pick, hist, csteps, cdt, cnt, crej = cpu_baseline(bg, y0, args.cpu_rays, args.cpu_days)
             evals = 6.0 * (csteps + crej) / max(csteps, 1)     # FSAL: 6 RHS columns per attempt
@@ -416,15 +575,52 @@ def main():
         dist.destroy_process_group()
 
 
-def main_c5(args, dist, group, rank, world, dev):
+def c5_parity_sample(eng, rows_all, fields, dev):
+    """The C5 line's parity check: the 4 096-ray sample of
+    tests/golden/c5_ref10_<storage>.npz (the oracle's TimeVaryingBackground,
+    tools/make_c5_ref.py) integrated 10 days (41 levels) on this engine; every
+    row must hash like the oracle's.  fp32 arithmetic (fp32a) is not the
+    reference's: its positions are compared with the fp64 fixture instead."""
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    from make_devmath import row_hashes
+    g = np.load(os.path.join(ROOT, "tests", "golden", f"c5_ref10_{'fp64' if fields != 'fp32' else 'fp32'}.npz"))
+    nt = int(g["nt"])
+    idx = torch.as_tensor(g["idx"], device=dev)
+    if rows_all.shape[1] != int(g["nslot"]):
+        return {"skipped": "the sample indexes the 5-period C5 set"}
+    r0 = rows_all[:, idx]
+    got = {}
+    eng.integrate(r0[:5].contiguous(), nt, 7200.0, ttotal=(nt - 1) * 7200.0, chunk=48,
+                  sink=lambda a, b, o: got.__setitem__(a, o[:, :, :7].cpu().numpy().copy()))
+    hist = np.full((7, nt, idx.numel()), np.nan)
+    hist[:, 0] = r0.cpu().numpy()
+    for a in sorted(got):
+        hist[:, a:a + got[a].shape[1]] = np.transpose(got[a], (2, 1, 0))
+    out = {"rays": int(idx.numel()), "rows": nt, "levels": int(g["nlev"]),
+           "fixture": f"tests/golden/c5_ref10_{'fp64' if fields != 'fp32' else 'fp32'}.npz"}
+    if fields == "fp32a":
+        last = g["last"]
+        ok = ~np.isnan(last[0]) & ~np.isnan(hist[0, -1])
+        d = np.max(np.abs(hist[:2, -1, ok] - last[:2, ok]), axis=0) if ok.any() else np.zeros(1)
+        out.update(vs="fp64-arithmetic oracle (fp32 RHS is not the reference's arithmetic)",
+                   p50=float(np.median(d)), p99=float(np.percentile(d, 99)), max=float(d.max()),
+                   alive_mismatch=int(np.sum(np.isnan(last[0]) != np.isnan(hist[0, -1]))))
+    else:
+        bad = int(np.sum(row_hashes(hist) != g["row_sha"]))
+        out.update(rows_identical=nt - bad, bitwise=bad == 0)
+    return out
+
+
+def main_c5(args, dist, group, rank, world, dev, share=1):
     """BASELINE configs[4]: a 0.25-degree time-varying background (one level
     every 6 h, built on the device by rwrt_bs_ready, fp64 or fp32 storage) and
     1-degree global seeds x k = 1..10 x ``--c5-periods`` of the C3 periods,
     90 days at 2 h.  One step = GPU initial rows + the time-varying ray loop
-    over the whole set, split across the ranks like C3/C4 (run_sharded:
-    probe, cost-balanced split, gather of endpoints + counters); levels and
-    sources are resident in HBM before the timed region (each rank builds
-    the same levels from the same synthetic snapshots)."""
+    over the whole set (weak scaling: every rank its own C5 set, the seed grid
+    shifted by rank x 1/N degree of longitude; strong: one set split like
+    C3/C4, run_sharded); levels and sources are resident in HBM before the
+    timed region (each rank builds the same levels from the same synthetic
+    snapshots)."""
     from engine import RayEngine
     from levels import Levels
     from shard import run_sharded
@@ -444,7 +640,9 @@ def main_c5(args, dist, group, rank, world, dev):
     cfg = S.config("C5")
     deg2rad = np.pi / 180.0
     ix, iy = np.meshgrid(np.arange(cfg.nnx), np.arange(cfg.nny))
-    lon = ((cfg.SW_lon % 360.0 + ix.ravel() * cfg.dlon) % 360.0) * deg2rad
+    weak = args.scaling == "weak"
+    offset = rank * cfg.dlon / world if weak else 0.0
+    lon = (((cfg.SW_lon + offset) % 360.0 + ix.ravel() * cfg.dlon) % 360.0) * deg2rad
     lat = (cfg.SW_lat + iy.ravel() * cfg.dlat) * deg2rad
     src = eng.sources(lon, lat)
     periods = S.C3_PERIODS_DAYS[: args.c5_periods]
@@ -464,14 +662,18 @@ def main_c5(args, dist, group, rank, world, dev):
     # rows per launch (measured, profiles/r1/c5/chunk_sweep.txt and
     # profiles/r1/v7/c5/): fp64 levels want a short time window (4 days: 17
     # levels in flight), fp32 levels 20-day windows
-    n_local = -(-nslot // world) + 2
-    free = torch.cuda.mem_get_info(dev)[0]
+    n_local = nslot if weak else -(-nslot // world) + 2
+    free = torch.cuda.mem_get_info(dev)[0] // share
     cap = max(1, min(nt - 1, int(0.8 * free) // (n_local * 64)))
     chunk = min(args.chunk or (240 if lv.fp32 else 48), cap)
     out = torch.empty((n_local, min(chunk, nt - 1), 8), dtype=torch.float64, device=dev)
     lead = [int(x) for x in str(args.first_chunk).split(",") if x]
 
     def one_step(events=None):
+        if weak:
+            return run_sharded(eng, make_y0(), nt, 7200.0, rank=0, world=1, probe=args.probe, lead=lead,
+                               chunk=chunk, out=out, events=events, ttotal=(nt - 1) * 7200.0,
+                               order_policy=args.order)
         return run_sharded(eng, make_y0(), nt, 7200.0, group=group, probe=args.probe, lead=lead,
                            chunk=chunk, out=out, events=events, ttotal=(nt - 1) * 7200.0,
                            order_policy=args.order)
@@ -496,7 +698,8 @@ def main_c5(args, dist, group, rank, world, dev):
     rej = int(r.res.nrej.sum().item())
     tot_steps, max_el, tot_rej = steps_done, elapsed, rej
     if dist:
-        t = torch.tensor([float(steps_done), elapsed, float(rej)], dtype=torch.float64, device=dev)
+        t = torch.tensor([float(steps_done), elapsed, float(rej)], dtype=torch.float64,
+                         device=dev if dist.get_backend() == "nccl" else "cpu")
         s, m = t.clone(), t.clone()
         dist.all_reduce(s, op=dist.ReduceOp.SUM)
         dist.all_reduce(m, op=dist.ReduceOp.MAX)
@@ -510,17 +713,23 @@ def main_c5(args, dist, group, rank, world, dev):
                     f"0.25deg time-varying background ({nlev} levels every 6 h, {args.fields} storage; "
                     f"BASELINE configs[4])")
         schedule = [args.probe] + [b - a for a, b in r.res.bounds]
+        del out
+        torch.cuda.empty_cache()
+        parity = c5_parity_sample(eng, torch.cat([x.reshape(7, -1) for x in rows], dim=1), args.fields, dev) \
+            if args.days >= 10 else {"skipped": "needs --days >= 10 (the fixture's horizon)"}
         print(json.dumps({
             "metric": METRIC, "value": tot_steps / max_el, "unit": "ray-steps/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * max_el / args.steps,
-            "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+            "higher_is_better": True, "scaling": "weak" if weak else "strong", "vs_baseline": None,
             "dtype": "f32 RHS, f64 stepper" if args.fields == "fp32a" else "f64",
             "data": "synthetic",
             "config": {"workload": workload, "ray_slots": nslot, "live_rays": n_live,
                        "rows": nt, "levels": nlev, "field_storage": args.fields,
                        "level_bytes": int(lv.packed[0].numel() * lv.packed.element_size()),
                        "rows_per_launch": chunk, "launch_rows": schedule,
-                       "parallelism": f"one ray set over {world} GPU(s) (run_sharded, as C3/C4)"},
+                       "parallelism": (f"{world} rank(s), each its own C5 seed grid (shifted by rank/N deg)"
+                                       if weak else f"one ray set over {world} GPU(s) (run_sharded, as C3/C4)")},
+            "parity_sample_vs_oracle": parity,
             "ray_steps_per_step": tot_steps / args.steps,
             "rejected_per_accepted": tot_rej * args.steps / max(tot_steps, 1),
             "levels_build_s": t_build,
@@ -533,4 +742,4 @@ def main_c5(args, dist, group, rank, world, dev):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -2550,6 +2550,10 @@ __device__ __forceinline__ void quad_rays(const RunArgs<StaticBG>& a, char* cach
   const int64_t w = qi * waves + blockIdx.x * 4 + (threadIdx.x >> 6);
   const int64_t ray = (qi < a.quad_per_wave && w < a.n_heavy) ? a.order[w] : -1;
   if (ray < 0) return;   // (whole quads: the four lanes share w)
+  // a ray frozen at the launch start is frozen_fill_kernel's (the C ABI asks
+  // for live rays in order[0, n_heavy); a C caller's frozen one is skipped
+  // here, not written twice)
+  if (a.frozen && a.frozen[ray]) return;
   double y[5], f[5], aux[3];
 #pragma unroll
   for (int v = 0; v < 5; ++v) {
@@ -3768,15 +3772,19 @@ rwrt_status launch_run(rwrt_ctx* ctx, const BG& B, int64_t nray, const rwrt_para
   if (n_heavy > 0 && !d_order) return fail(RWRT_ERR_ARG, "n_heavy > 0 needs d_order%s");
   if (n_heavy > 0 && !std::is_same<BG, StaticBG>::value)
     return fail(RWRT_ERR_ARG, "latency mode (n_heavy > 0) runs on the static background only%s");
+  // the context's settings are read once, under its lock: a concurrent
+  // rwrt_ctx_set_latency_density cannot change the density between sizing the
+  // latency-mode grid and launching it
+  std::lock_guard<std::mutex> lock(ctx->mu);
 #if RWRT_LATENCY_QUAD
-  const int64_t per_block = 4 * (int64_t)ctx->quad_per_wave;   // rays per latency-mode block
+  const int32_t quad_per_wave = ctx->quad_per_wave;
+  const int64_t per_block = 4 * (int64_t)quad_per_wave;   // rays per latency-mode block
 #else
   const int64_t per_block = kTeamLanes;
 #endif
   const int64_t team_blocks = (n_heavy + per_block - 1) / per_block;
   if (team_blocks > ctx->ncu / 2)
     return fail(RWRT_ERR_ARG, "n_heavy exceeds the latency mode's capacity (4 x rays-per-wave per CU, half the CUs)%s");
-  std::lock_guard<std::mutex> lock(ctx->mu);
   DeviceGuard dg(ctx->device);
   if (!dg.ok) return check_launch("hipSetDevice(context device)");
   hipStream_t st = (hipStream_t)stream;
@@ -3809,7 +3817,7 @@ rwrt_status launch_run(rwrt_ctx* ctx, const BG& B, int64_t nray, const rwrt_para
   // hardware queues' dispatch order (a second kernel on another stream could
   // wait for a CU on its XCD until the persistent grid drains)
   a.heavy_blocks = (int32_t)team_blocks;
-  a.quad_per_wave = ctx->quad_per_wave;
+  a.quad_per_wave = quad_per_wave;
   if (nray > n_heavy || team_blocks) {
     const int64_t grid = team_blocks + (nray > n_heavy ? blocks : 0);
     hipLaunchKernelGGL(rk45_run_kernel<BG>, dim3((unsigned)grid), dim3(256), 0, st, a);

@@ -502,27 +502,41 @@ class RayEngine:
         res = RunResult(cnt[:, 0], cnt[:, 1], st["nanrow"], False, brk, n_live)
         res.bounds = bounds
         res.state, res.next_row = st, end
+        res.params = run_params(p, tb)
         return res
 
     # ------------------------------------------------------ checkpoint / resume
+    CHECKPOINT_KEYS = {"state", "count", "nanrow", "next_row", "params", "nray"}
+
     @staticmethod
     def checkpoint(res):
         """The solver state after the rows a run produced (the
         state is 12 fp64 + 3 integers per ray, so resuming = persisting it at an
-        output index): host arrays that ``resume`` continues from bit for bit."""
+        output index): host arrays that ``resume`` continues from bit for bit,
+        with the run's parameters (``run_params``: rtol, atol, min step,
+        cut-off, nt, tstep, last output time) and ray count, which ``resume``
+        checks."""
         st = res.state
         return {"state": st["state"].cpu().numpy(), "count": st["count"].cpu().numpy(),
-                "nanrow": st["nanrow"].cpu().numpy(), "next_row": np.int64(res.next_row)}
+                "nanrow": st["nanrow"].cpu().numpy(), "next_row": np.int64(res.next_row),
+                "params": np.asarray(res.params, np.float64), "nray": np.int64(st["nray"])}
+
+    @staticmethod
+    def _ck_path(path):
+        p = os.fspath(path)
+        return p if p.endswith(".npz") else p + ".npz"   # (np.savez appends .npz)
 
     @staticmethod
     def save_checkpoint(ck, path):
-        np.savez(path, **ck)
+        np.savez(RayEngine._ck_path(path), **ck)
 
     @staticmethod
     def load_checkpoint(path):
+        path = RayEngine._ck_path(path)
         with np.load(path, allow_pickle=False) as z:
             ck = {k: z[k] for k in z.files}
-        if set(ck) != {"state", "count", "nanrow", "next_row"} or ck["state"].shape[0] != H.NSTATE:
+        if (set(ck) != RayEngine.CHECKPOINT_KEYS or ck["state"].shape[0] != H.NSTATE
+                or ck["state"].shape[1] != int(ck["nray"]) or ck["params"].shape != (7,)):
             raise ValueError(f"{path}: not an rwrt checkpoint")
         return ck
 
@@ -535,6 +549,13 @@ class RayEngine:
         p = self.params(nt, tstep, rtol, atol, msf, cut_off, cut_rad)
         tb = torch.as_tensor(t_eval_of(nt, tstep, ttotal), dtype=F64, device=self.device)
         nray = int(ck["state"].shape[1])
+        want = np.asarray(ck["params"], np.float64)
+        got = np.asarray(run_params(p, tb), np.float64)
+        if not np.array_equal(want, got) or nray != int(ck["nray"]):
+            names = ["rtol", "atol", "min_step", "cut_off", "nt", "tstep", "t_last"]
+            diff = {n: (float(a), float(b)) for n, a, b in zip(names, want, got) if a != b}
+            raise ValueError(f"checkpoint taken with other run parameters {diff} (checkpoint, resume): "
+                             f"the continuation would not equal the uninterrupted run")
         st = dict(state=torch.as_tensor(ck["state"], dtype=F64).to(self.device).contiguous(),
                   count=torch.as_tensor(ck["count"], dtype=torch.int64).to(self.device).contiguous(),
                   nanrow=torch.as_tensor(ck["nanrow"], dtype=torch.int32).to(self.device).contiguous(),
@@ -559,6 +580,12 @@ class RayEngine:
         """Live-first queue order from the state itself (NaN mean = frozen)."""
         dead = torch.isnan(st["state"][:5].sum(0)).to(torch.int8)
         return torch.sort(dead, stable=True).indices.to(torch.int64).contiguous()
+
+
+def run_params(p, tb):
+    """The parameters a run's continuation depends on (checkpoints carry them):
+    ``[rtol, atol, min_step, cut_off, nt, tstep, last output time]``."""
+    return [p.rtol, p.atol, p.min_step, p.cut_off, float(p.nt), p.tstep, float(tb[-1].item())]
 
 
 def _row_buffers(out, nray, rows_max, device):

@@ -41,16 +41,27 @@ import torch
 import _hip as H
 
 F64 = torch.float64
-_PINNED = {}
+_PINNED = {}            # n -> free pairs of page-locked staging buffers
+_PINNED_LOCK = threading.Lock()
 
 
-def _pinned(n):
-    """Two page-locked staging buffers of ``n`` doubles, kept across runs
-    (pinning is slow)."""
-    if n not in _PINNED:
-        _PINNED.clear()
-        _PINNED[n] = [torch.empty(n, dtype=F64, pin_memory=True) for _ in range(2)]
-    return _PINNED[n]
+def _pinned_take(n):
+    """Two page-locked staging buffers of ``n`` doubles for ONE sink: checked
+    out of a free list (pinning is slow, so released pairs are reused by the
+    next run), never shared by two live sinks -- two runs in two threads (two
+    GPUs, two contexts) would otherwise overwrite each other's D2H data."""
+    with _PINNED_LOCK:
+        free = _PINNED.get(n)
+        if free:
+            return free.pop()
+        if sum(len(v) for v in _PINNED.values()) > 2:
+            _PINNED.clear()    # keep at most a few idle pairs pinned
+    return [torch.empty(n, dtype=F64, pin_memory=True) for _ in range(2)]
+
+
+def _pinned_release(n, pair):
+    with _PINNED_LOCK:
+        _PINNED.setdefault(n, []).append(pair)
 
 
 def fill_rows(dst, prev, src, cols):
@@ -75,7 +86,8 @@ class HistorySink:
         self.workers = workers
         self.copy_stream = torch.cuda.Stream(device=device)
         self.stage_dev = [torch.empty(7 * max_rows * nray, dtype=F64, device=device) for _ in range(2)]
-        self.stage_host = _pinned(7 * max_rows * nray)
+        self.stage_n = 7 * max_rows * nray
+        self.stage_host = _pinned_take(self.stage_n)
         self.out = [torch.empty((nray, max_rows, 8), dtype=F64, device=device) for _ in range(2)]
         # row 0 (the host initial rows) is every ray's "previous row" of chunk 1
         row0 = np.stack([np.ascontiguousarray(h[0]).reshape(-1) for h in hist], axis=1)
@@ -185,3 +197,6 @@ class HistorySink:
                 f.result()
         self.copy_stream.synchronize()
         self.pool.shutdown(wait=True)
+        if self.stage_host is not None:
+            _pinned_release(self.stage_n, self.stage_host)
+            self.stage_host = None

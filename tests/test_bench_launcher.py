@@ -1,0 +1,62 @@
+"""bench.py's N-GPU launcher (CPU): ``--gpus N`` without a launcher starts N
+ranks itself; under torch.distributed.run it checks N against WORLD_SIZE.
+
+The driver runs ``python bench.py --gpus N`` (or the same under
+torch.distributed.run); either must give an N-rank run whose rank 0 prints
+one line with ``n_gpus: N`` (``--gpus`` used to be ignored).
+``--dry-run`` stops after the process group is up, so the spawn path is
+tested end to end here with gloo (no GPU).
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def test_resolve_world_rules():
+    from bench import resolve_world
+    assert resolve_world(None, {}) == ("rank", 1)
+    assert resolve_world(1, {}) == ("rank", 1)
+    assert resolve_world(8, {}) == ("spawn", 8)
+    assert resolve_world(4, {"WORLD_SIZE": "4"}) == ("rank", 4)
+    assert resolve_world(None, {"WORLD_SIZE": "2"}) == ("rank", 2)
+    with pytest.raises(SystemExit):
+        resolve_world(8, {"WORLD_SIZE": "2"})          # --gpus disagrees with the launcher
+    with pytest.raises(SystemExit):
+        resolve_world(0, {})
+
+
+def _bench(args, env_extra=None, timeout=240):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="", **(env_extra or {}))
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env, cwd=ROOT,
+                       capture_output=True, text=True, timeout=timeout)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    return p, lines
+
+
+def test_gpus2_spawns_two_ranks_one_line():
+    p, lines = _bench(["--gpus", "2", "--dry-run"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert len(lines) == 1, p.stdout                # rank 0 alone prints
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["world_sum"] == 2.0 and d["backend"] == "gloo"
+    assert d["scaling"] == "weak"
+
+
+def test_gpus_mismatch_under_launcher_fails_loudly():
+    p, lines = _bench(["--gpus", "4", "--dry-run"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert p.returncode != 0 and not lines
+    assert "WORLD_SIZE=2" in p.stderr
+
+
+def test_failing_rank_ends_the_run():
+    # an unreachable rendezvous makes every rank fail: the parent must return
+    # non-zero instead of hanging
+    p, lines = _bench(["--gpus", "2", "--dry-run"], {"RWRT_DIST_BACKEND": "no_such_backend"})
+    assert p.returncode != 0 and not lines

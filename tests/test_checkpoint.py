@@ -20,14 +20,19 @@ def test_checkpoint_file_roundtrip(tmp_path):
     from engine import RayEngine
     rng = np.random.default_rng(0)
     ck = {"state": rng.standard_normal((12, 7)), "count": rng.integers(0, 9, (7, 2)),
-          "nanrow": np.full(7, 121, np.int32), "next_row": np.int64(37)}
-    path = os.path.join(tmp_path, "ck.npz")
-    RayEngine.save_checkpoint(ck, path)
-    got = RayEngine.load_checkpoint(path)
-    for k in ck:
-        assert np.array_equal(got[k], ck[k]) and got[k].dtype == np.asarray(ck[k]).dtype
+          "nanrow": np.full(7, 121, np.int32), "next_row": np.int64(37),
+          "params": np.array([1e-6, 1e-6, 7.2, 0.2, 121.0, 7200.0, 864000.0]), "nray": np.int64(7)}
+    for name in ("ck.npz", "ck"):                 # np.savez appends .npz: the same path loads
+        path = os.path.join(tmp_path, name)
+        RayEngine.save_checkpoint(ck, path)
+        got = RayEngine.load_checkpoint(path)
+        for k in ck:
+            assert np.array_equal(got[k], ck[k]) and got[k].dtype == np.asarray(ck[k]).dtype
     bad = os.path.join(tmp_path, "bad.npz")
     np.savez(bad, state=np.zeros((5, 3)))
+    with pytest.raises(ValueError):
+        RayEngine.load_checkpoint(bad)
+    np.savez(bad, **dict(ck, nray=np.int64(8)))   # ray count and state disagree
     with pytest.raises(ValueError):
         RayEngine.load_checkpoint(bad)
 
@@ -69,3 +74,6 @@ def test_resume_equals_uninterrupted(tmp_path):
     assert a.shape == b.shape and np.array_equal(a.view(np.int64), b.view(np.int64))
     assert torch.equal(r2.nacc, rf.nacc) and torch.equal(r2.nrej, rf.nrej)
     assert torch.equal(r2.nanrow, rf.nanrow)
+    # a resume with other run parameters is refused, not silently different
+    with pytest.raises(ValueError, match="rtol"):
+        eng2.resume(RayEngine.load_checkpoint(path), nt, 7200.0, rtol=1e-5, chunk=24)

@@ -67,6 +67,7 @@ def c3_run():
     return _C3["gpu"]
 
 
+@pytest.mark.refhost
 def test_c3_sample_bitwise_with_reference_arithmetic():
     import rwrt_oracle as O
     hist, nacc, y0, bg, nt = c3_run()
@@ -148,6 +149,7 @@ def test_c4_cost_sharded_world2_equals_single_gpu():
     assert same(ends, hist[:, -1])
 
 
+@pytest.mark.refhost
 # ---------------------------------------------------------------- C5
 @pytest.mark.parametrize("fp32", [False, True])
 def test_c5_025deg_bitwise_with_oracle(fp32):

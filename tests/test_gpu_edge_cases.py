@@ -16,7 +16,7 @@ import torch
 from conftest import golden
 import synthetic as S
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.refhost]
 NT = 25
 
 

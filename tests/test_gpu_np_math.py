@@ -13,7 +13,7 @@ host on arguments that exercise them.
 import numpy as np
 import pytest
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.refhost]
 
 
 def bitwise(a, b):

@@ -142,6 +142,7 @@ def test_initial_rows_gpu_bitwise_c3_golden(kind):
         assert same_bits(got, g[f"{tag}_{kind}_rows"]), tag
 
 
+@pytest.mark.refhost
 @pytest.mark.parametrize("kind", KINDS)
 def test_initial_rows_gpu_equals_host_full_c3(kind):
     """All 2.40 M C3 slots (5 periods): GPU rows == host rows (the host path is

@@ -58,6 +58,7 @@ def test_rk4_c2_90d_bitwise_with_reference_arithmetic(kind):
     check_rows(row_hashes(hist), g["rk4_row_sha"], hist, g["rk4_last"])
 
 
+@pytest.mark.refhost
 @pytest.mark.parametrize("fp32", [False, True])
 def test_time_varying_c2_bitwise_with_oracle(fp32):
     """The time-varying path (fp64 levels: one level in the LDS cache, the

@@ -36,6 +36,7 @@ def rows_of(eng, y0, nt, **kw):
     return np.concatenate([rows[k] for k in sorted(rows)], axis=1), res
 
 
+@pytest.mark.refhost
 def test_team_c3_sample_bitwise_with_reference_arithmetic():
     import rwrt_oracle as O
     from bench import c3_initial_state, make_bs

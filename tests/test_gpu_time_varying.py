@@ -22,7 +22,7 @@ import rwrt_oracle as O
 import synthetic as S
 from conftest import GOLDEN
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.refhost]
 
 HOT = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 11]
 DT = 6 * 3600.0
