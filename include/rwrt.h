@@ -261,9 +261,7 @@ rwrt_status rwrt_kat_rk45(int32_t kind, int64_t ncol, const double* d_y0,
  * by the earth radius), 12 fmod(x, y) for y > 0 (the kernels' exact fmod),
  * 13 x % (2 pi) and 14 (x % (2 pi)) % (2 pi) as the kernels evaluate them,
  * 15 x / y by a shared reciprocal, 16 np.floor(x).astype(int32),
- * 17/18/19 sin/cos/tan from the fused one-reduction routine, 20 pow(x, y) and
- * 21 exp(x) as restated in csrc/rwrt_math.h, 22 the refined reciprocal
- * (v_rcp_f64 + two Newton steps) of x, 23/24 x / y through the interleaved
+ * (17-22: retired device-libm restatements), 23/24 x / y through the interleaved
  * division pair (as its first / second quotient), 25/26/27/28 the reference
  * NumPy's sin/cos/tan/power as restated in csrc/np_math.h, 29 the restated
  * VRCP14PD, 30/31/32 sin/cos/tan and 33 pow exactly as the kernels evaluate

@@ -33,52 +33,14 @@ constexpr double kHalfPi = 0.5 * kPi;  // "0.5 * pi"  wr.py:508, bs.py:787
 constexpr double kTwoPi = 2.0 * kPi;   // "2 * pi"    bs.py:519, interpolation.py:80
 constexpr double kREarth = 6.3712e6;
 constexpr double kOmega = 7.2921e-5;   // constants.py omega
-constexpr double kRInv = 1.0 / 6.3712e6;   // RN(1 / R)
 
-// x / R correctly rounded without the division sequence (Markstein): q0 is
-// within an ulp of x/R, the FMA remainder r = x - q0 R is exact, and one more
-// FMA rounds q0 + r/R correctly.  Zero, tiny, huge and non-finite x take the
-// IEEE division (signed zeros, gradual underflow).  Verified bit-exact against
-// IEEE division on the device (tests/test_gpu_parity.py).
-// A zero x stays on the fast path (q0 = x * RN(1/R) is the correctly signed
-// zero, kept by the copysign): in a zonal flow dk/dt is exactly -0 for every
-// ray, so the fallback would otherwise run on every evaluation.
-#ifndef RWRT_RHS_TRIG_SMALL
-#define RWRT_RHS_TRIG_SMALL 1
-#endif
-#ifndef RWRT_TRIG_EARLY
-#define RWRT_TRIG_EARLY 1   // the RHS trigonometry's first half before the lookup's refill branch
-#endif
-#ifndef RWRT_DIV_REARTH_IEEE
-#define RWRT_DIV_REARTH_IEEE 1
-#endif
-__device__ __forceinline__ double div_rearth(double x) {
-#if RWRT_DIAG_NODIV
-  return x * kRInv;
-#elif RWRT_DIV_REARTH_IEEE
-  return x / kREarth;
-#endif
-  const double ax = fabs(x);
-  const double q0 = x * kRInv;
-  const double r = fma(-q0, kREarth, x);
-  double q = copysign(fma(r, kRInv, q0), q0);
-  if (!(ax < 0x1p900) | ((ax < 0x1p-900) & (ax != 0.0))) {
-    asm volatile("");   // tiny, huge, infinite or NaN: IEEE division (rare branch)
-    q = x / kREarth;
-  }
-  return q;
-}
+// x / R (wr.py:80-82), IEEE
+__device__ __forceinline__ double div_rearth(double x) { return x / kREarth; }
 constexpr double kNaN = __builtin_nan("");
 
 // Output rows are written once and never read back by the kernels: stores
 // marked non-temporal stream past the L2 instead of evicting the basic state
 // and solver state the ray loop re-reads.
-#ifndef RWRT_NT_ROWS
-#define RWRT_NT_ROWS 0
-#endif
-#ifndef RWRT_NT_FILL
-#define RWRT_NT_FILL 1
-#endif
 typedef double v2f64 __attribute__((ext_vector_type(2)));
 template <bool NT>
 __device__ __forceinline__ void store_row16(double2* o, double2 v) {
@@ -102,15 +64,8 @@ __device__ __forceinline__ void store_row16(double2* o, double2 v) {
 // sequential: A's flag is written early (it only needs the inputs) and read
 // 5 instructions later; B's is written after A's v_div_fmas and read after
 // 3 instructions + 1 wait state (4 are required).
-#ifndef RWRT_DIV2_ASM
-#define RWRT_DIV2_ASM 1
-#endif
 __device__ __forceinline__ void div2(double a1, double b1, double a2, double b2, double& qa,
                                      double& qb) {
-#if RWRT_DIAG_NODIV   // timing-only diagnostic build: approximate quotients
-  qa = a1 * __builtin_amdgcn_rcp(b1);
-  qb = a2 * __builtin_amdgcn_rcp(b2);
-#elif RWRT_DIV2_ASM
   double dA, dB, rA, rB, eA, eB, nA, nB;
   asm(
       "v_div_scale_f64 %[dA], vcc, %[bA], %[bA], %[aA]\n\t"
@@ -140,16 +95,7 @@ __device__ __forceinline__ void div2(double a1, double b1, double a2, double b2,
         [rB] "=&v"(rB), [eA] "=&v"(eA), [eB] "=&v"(eB), [nA] "=&v"(nA), [nB] "=&v"(nB)
       : [aA] "v"(a1), [bA] "v"(b1), [aB] "v"(a2), [bB] "v"(b2)
       : "vcc");
-#else
-  qa = a1 / b1;
-  qb = a2 / b2;
-#endif
 }
-#if RWRT_DIAG_NODIV   // timing-only diagnostic build: approximate quotients in the RHS
-#define RDIV(a, b) ((a) * __builtin_amdgcn_rcp(b))
-#else
-#define RDIV(a, b) ((a) / (b))
-#endif
 
 // rkf45.py:604-615 (Dormand-Prince 5(4)); C++ constant division is IEEE
 // correctly rounded, like Python's.
@@ -198,12 +144,10 @@ __device__ __forceinline__ double fmod_pos(double a, double b, double binv = 0.0
   double r = fma(-n, b, x);
   const double lo = r + b, hi = fma(-(n + 1.0), b, x);
   r = (r < 0.0) ? lo : ((r >= b) ? hi : r);
-#if !RWRT_DIAG_FMOD_NOFALLBACK
   if (!(x < 0x1p40)) {
     asm volatile("");   // NaN, inf, huge: library routine (rare branch)
     r = fabs(fmod(a, b));
   }
-#endif
   return copysign(r, a);
 }
 
@@ -269,18 +213,6 @@ __device__ __forceinline__ double div_hw(double a, double b, double rb) {
   }
   return r;
 }
-// x / c for a wave-uniform c: the reciprocal is loop-invariant (hoisted to
-// the kernel entry)
-#ifndef RWRT_CELL_DIV_IEEE
-#define RWRT_CELL_DIV_IEEE 1
-#endif
-__device__ __forceinline__ double div_uniform(double x, double c) {
-#if RWRT_CELL_DIV_IEEE
-  return x / c;
-#else
-  return div_hw(x, c, recip_hw(c));
-#endif
-}
 
 // ---------------------------------------------------------------------------
 // Basic state: packed [W][H][12] fp64, the 11 hot fields of BS.fields
@@ -290,13 +222,6 @@ constexpr int kNF = RWRT_NFIELD_PACK;
 // slot -> index in the reference 18-field stack (bs.py:349-368); qyx (10) and
 // the six third derivatives are never read on the hot path.
 __constant__ int kRefIndex[11] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 11};
-
-#ifndef RWRT_STAGE_BARRIER
-#define RWRT_STAGE_BARRIER 0
-#endif
-#ifndef RWRT_INTERP_GROUP
-#define RWRT_INTERP_GROUP 2   // records (of 2 fields) per load group, divides 6
-#endif
 
 struct Field {
   const double* __restrict__ P;
@@ -366,14 +291,14 @@ __device__ __forceinline__ void interp11(const Field& F, double lon, double lat,
   // Three groups of 2 records x 4 corners: bounds the registers held by
   // in-flight loads (the lookup is L2-resident; occupancy hides the latency).
 #pragma unroll
-  for (int q0 = 0; q0 < 6; q0 += RWRT_INTERP_GROUP) {
+  for (int q0 = 0; q0 < 6; q0 += 2) {
 #pragma unroll
-    for (int q = q0; q < q0 + RWRT_INTERP_GROUP; ++q) {
+    for (int q = q0; q < q0 + 2; ++q) {
       const double2 va = pa[q], vb = pb[q], vc = pc[q], vd = pd[q];
       g[2 * q] = blend(k, va.x, vb.x, vc.x, vd.x);
       if (2 * q + 1 < 11) g[2 * q + 1] = blend(k, va.y, vb.y, vc.y, vd.y);
     }
-    if (q0 + RWRT_INTERP_GROUP < 6) __builtin_amdgcn_sched_barrier(0);
+    if (q0 + 2 < 6) __builtin_amdgcn_sched_barrier(0);
   }
 }
 
@@ -447,34 +372,14 @@ __device__ __forceinline__ void lookup_end(const BG& B, const PendingPoint& p, d
 // the fill's latency overlaps the trigonometry; end() waits for it.  Same
 // values, same blend: results are unchanged.
 //
-// Slice layout of the time-varying caches (LDS-DMA writes wave base + lane *
-// 16 B): per wave, chunk (corner j, record q) of all 64 lanes at wave_base +
-// (j * 6 + q) * 1 KiB -- a refill is 24 LDS-DMA instructions for the wave.
-// The static cache (RWRT_CACHE_LANE_SLICE) keeps each lane's 24 chunks
-// contiguous instead, at wave_base + lane * 400 B (384 B + 16 B of padding:
-// lanes 16 apart start 64 banks apart, so 16 lanes' ds_read_b128 are
-// conflict-free): the refill of one lane is ONE LDS-DMA instruction whose 24
-// lanes fetch that lane's 24 chunks (refill_lane_slice), so a wave pays an
-// instruction per lane that missed instead of 24 whenever any lane missed.
-// Measured on C3 (profiles/r2/ab/lane_slice.txt): 3.13e9 against 3.44e9 for
-// the chunk-major layout -- the per-lane refill sequence (readlanes, an exec
-// swap, the select and M0 set-up, ~25 instructions) outweighs the 24 LDS-DMA
-// issues it replaces (~21 cycles each, tools/probes/lat_probe.hip) once a
-// few lanes of a wave miss together (every ray a lane pulls starts with a
-// miss), so it is off by default.
-#ifndef RWRT_CELL_CACHE
-#define RWRT_CELL_CACHE 1
-#endif
-#ifndef RWRT_CACHE_LANE_SLICE
-#define RWRT_CACHE_LANE_SLICE 0
-#endif
-#ifndef RWRT_DMA_WAIT_IF
-#define RWRT_DMA_WAIT_IF 0   // wait for the refill's LDS-DMA only when the wave issued one
-#endif
+// Slice layout (LDS-DMA writes wave base + lane * 16 B): per wave, chunk
+// (corner j, record q) of all 64 lanes at wave_base + (j * 6 + q) * 1 KiB --
+// a refill is 24 LDS-DMA instructions for the wave.  (A lane-major layout with
+// one LDS-DMA per missing lane measured 0.91x on C3: every ray a lane pulls
+// starts with a miss, so several lanes of a wave miss together;
+// profiles/r2/ab/lane_slice.txt.)
 constexpr int kCacheChunks = 4 * 6;                        // 4 corners x 6 x 16 B
 constexpr int kCacheBytesPerWave = kCacheChunks * 64 * 16;  // 24 KiB
-constexpr int kSliceStride = 400;                          // bytes per lane (lane-slice layout)
-constexpr int kStaticCacheBytesPerWave = RWRT_CACHE_LANE_SLICE ? 64 * kSliceStride : kCacheBytesPerWave;
 typedef __attribute__((address_space(3))) void* lds_void_ptr;
 typedef __attribute__((address_space(1))) const void* global_void_ptr;
 
@@ -482,18 +387,11 @@ typedef __attribute__((address_space(1))) const void* global_void_ptr;
 // base passed through an opaque SGPR copy, so that the compiler rebuilds the
 // 24 destinations with one s_add each instead of keeping 24 loop-invariant
 // M0 values live (they spill to VGPR lanes: v_readlane + s_mov per load).
-#ifndef RWRT_FRESH_M0
-#define RWRT_FRESH_M0 1
-#endif
 __device__ __forceinline__ char* lds_slice_base(char* wave_base) {
-#if RWRT_FRESH_M0
   typedef __attribute__((address_space(3))) char lds_char;
   unsigned b = (unsigned)(size_t)(lds_char*)wave_base;
   asm volatile("" : "+s"(b));
   return (char*)(lds_char*)(size_t)b;
-#else
-  return wave_base;
-#endif
 }
 
 // Before end() reads a slice: wait for the refill's LDS-DMA.  Explicit,
@@ -503,142 +401,23 @@ __device__ __forceinline__ char* lds_slice_base(char* wave_base) {
 // that carry scopes too -- which these (through lds_slice_base) do not.
 __device__ __forceinline__ void lds_dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-// Timing-only diagnostic build (RWRT_DIAG_STAMPS=1, tools/stamps.py): cycle
-// counts of the sections of an attempt, summed over the active lanes' waves
-// (one count per wave, from its first active lane: per-wave time, for a
-// single ray or a whole batch).  RWRT_STAMP(k) charges the cycles since the
-// previous stamp of the wave to section k.
-#ifndef RWRT_DIAG_STAMPS
-#define RWRT_DIAG_STAMPS 0
-#endif
-#if RWRT_DIAG_STAMPS
-__device__ unsigned long long g_stamp[16];
-__shared__ unsigned long long s_stamp_last[4];   // per wave of the block
-__shared__ unsigned long long s_stamp_acc[4][16];  // per wave, flushed at the kernel's end
-#define RWRT_STAMP(k)                                                        \
-  do {                                                                       \
-    const unsigned long long _t = __builtin_amdgcn_s_memtime();             \
-    const unsigned _w = (threadIdx.x >> 6) & 3;                              \
-    if (__lane_id() == __builtin_amdgcn_readfirstlane(__lane_id()))          \
-      s_stamp_acc[_w][k] += _t - s_stamp_last[_w];                           \
-    s_stamp_last[_w] = _t;                                                   \
-  } while (0)
-// (no global atomics inside the loop: they would sit in vmcnt and inflate the
-// LDS-DMA waits being measured)
-__device__ __forceinline__ void stamp_init() {
-  const unsigned w = (threadIdx.x >> 6) & 3;
-  if ((threadIdx.x & 63) < 16) s_stamp_acc[w][threadIdx.x & 63] = 0;
-  s_stamp_last[w] = __builtin_amdgcn_s_memtime();
-}
-__device__ __forceinline__ void stamp_flush() {
-  const unsigned w = (threadIdx.x >> 6) & 3;
-  if ((threadIdx.x & 63) < 16) atomicAdd(&g_stamp[threadIdx.x & 63], s_stamp_acc[w][threadIdx.x & 63]);
-}
-#else
-#define RWRT_STAMP(k) \
-  do {                \
-  } while (0)
-#endif
-
-#if RWRT_CACHE_LANE_SLICE
-// Refill lane L's slice (LDS address m0v) with the 24 chunks of its corners
-// (element offsets a, b, c, d from P): ONE global_load_lds_dwordx4 executed
-// by lanes 0..23 whatever the wave's exec mask -- lane i fetches chunk i =
-// (corner i / 6, record i % 6) into m0v + i * 16.  The exec mask is saved
-// and restored around it; the VGPRs written here are asm outputs (dead after
-// it), so no live value of an inactive lane is touched; M0 is restored.
-__device__ __forceinline__ void refill_lane_slice(unsigned m0v, unsigned a, unsigned b, unsigned c,
-                                                  unsigned d, const double* P) {
-  unsigned long long save;
-  unsigned save_m0, vo, vl, vt;
-  asm volatile(
-      "s_mov_b32 %[sm], m0\n\t"
-      "s_mov_b64 %[sv], exec\n\t"
-      "s_mov_b32 exec_lo, 0xffffff\n\t"
-      "s_mov_b32 exec_hi, 0\n\t"
-      "v_mbcnt_lo_u32_b32 %[vl], -1, 0\n\t"
-      "v_mbcnt_hi_u32_b32 %[vl], -1, %[vl]\n\t"
-      "v_mul_u32_u24 %[vt], 43, %[vl]\n\t"
-      "v_lshrrev_b32 %[vt], 8, %[vt]\n\t"          // lane / 6 (lanes < 64)
-      "v_mul_u32_u24 %[vt], 6, %[vt]\n\t"
-      "v_sub_u32 %[vl], %[vl], %[vt]\n\t"
-      "v_lshlrev_b32 %[vl], 4, %[vl]\n\t"          // (lane % 6) * 16 B
-      "v_mov_b32 %[vo], %[d]\n\t"
-      "v_mov_b32 %[vt], %[c]\n\t"
-      "v_cndmask_b32_e64 %[vo], %[vo], %[vt], %[mc]\n\t"
-      "v_mov_b32 %[vt], %[b]\n\t"
-      "v_cndmask_b32_e64 %[vo], %[vo], %[vt], %[mb]\n\t"
-      "v_mov_b32 %[vt], %[a]\n\t"
-      "v_cndmask_b32_e64 %[vo], %[vo], %[vt], %[ma]\n\t"
-      "v_lshl_add_u32 %[vo], %[vo], 3, %[vl]\n\t"    // corner offset * 8 B + chunk
-      "s_mov_b32 m0, %[dst]\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %[vo], %[P]\n\t"
-      "s_mov_b64 exec, %[sv]\n\t"
-      "s_mov_b32 m0, %[sm]"
-      : [sv] "=&s"(save), [sm] "=&s"(save_m0), [vo] "=&v"(vo), [vl] "=&v"(vl), [vt] "=&v"(vt)
-      : [a] "s"(a), [b] "s"(b), [c] "s"(c), [d] "s"(d), [ma] "s"(0x3Full), [mb] "s"(0xFC0ull),
-        [mc] "s"(0x3F000ull), [dst] "s"(m0v), [P] "s"(P)
-      : "memory");
-}
-#endif
-
 struct CachedStaticBG {
   static constexpr bool kTimeVarying = false;
   Field F;
   char* wave_base;                // this wave's slice area (wave-uniform)
-  unsigned lane16;                // lane * 16 (lane * kSliceStride with RWRT_CACHE_LANE_SLICE)
+  unsigned lane16;                // lane * 16
   mutable unsigned key_x, key_y;  // cell held in the slice (~0u: none)
 
   struct Pending {
     double wa, wb, wc, wd;
-    bool refilled;   // (wave-uniform) some lane of the wave refilled its slice
   };
   __device__ __forceinline__ const double2& chunk(int j, int q) const {
-#if RWRT_CACHE_LANE_SLICE
-    return *reinterpret_cast<const double2*>(wave_base + lane16 + (j * 6 + q) * 16);
-#else
     return *reinterpret_cast<const double2*>(wave_base + (j * 6 + q) * 1024 + lane16);
-#endif
   }
   __device__ __forceinline__ Pending begin(double lon, double lat) const {
     const Corners k = corners(F, py_mod_2pi(lon), lat);
-#if RWRT_CACHE_LANE_SLICE
     const bool miss = k.key_x != key_x || k.key_y != key_y;
-    unsigned long long m = __ballot(miss);   // the lanes that changed cell (wave-uniform)
-    if (m) {
-#if RWRT_DIAG_STAMPS
-      RWRT_STAMP(1);
-      if (__lane_id() == __builtin_amdgcn_readfirstlane(__lane_id())) s_stamp_acc[(threadIdx.x >> 6) & 3][11] += 1;
-#endif
-      typedef __attribute__((address_space(3))) char lds_char;
-      const unsigned base = (unsigned)(size_t)(lds_char*)wave_base;
-      do {
-        const int L = __builtin_ctzll(m);
-        m &= m - 1;
-        refill_lane_slice(base + (unsigned)L * kSliceStride, __builtin_amdgcn_readlane(k.oa, L),
-                          __builtin_amdgcn_readlane(k.ob, L), __builtin_amdgcn_readlane(k.oc, L),
-                          __builtin_amdgcn_readlane(k.od, L), F.P);
-      } while (m);
-      RWRT_STAMP(10);
-    }
-    if (miss) {
-      key_x = k.key_x;
-      key_y = k.key_y;
-    }
-    return Pending{k.wa, k.wb, k.wc, k.wd, true};
-#else
-    const bool miss = k.key_x != key_x || k.key_y != key_y;
-#if RWRT_DMA_WAIT_IF
-    const bool any = __ballot(miss) != 0;
-#else
-    const bool any = true;
-#endif
     if (miss) {   // miss: refill the slice by LDS-DMA
-#if RWRT_DIAG_STAMPS
-      RWRT_STAMP(1);
-      if (__lane_id() == __builtin_amdgcn_readfirstlane(__lane_id())) s_stamp_acc[(threadIdx.x >> 6) & 3][11] += 1;
-#endif
       const double* src[4] = {k.a, k.b, k.c, k.d};
       char* const base = lds_slice_base(wave_base);
 #pragma unroll
@@ -649,26 +428,16 @@ struct CachedStaticBG {
                                            (lds_void_ptr)(base + (j * 6 + q) * 1024), 16, 0, 0);
       key_x = k.key_x;
       key_y = k.key_y;
-      RWRT_STAMP(10);
     }
-    return Pending{k.wa, k.wb, k.wc, k.wd, any};
-#endif
+    return Pending{k.wa, k.wb, k.wc, k.wd};
   }
   __device__ __forceinline__ void end(const Pending& p, double g[11]) const {
-    RWRT_STAMP(2);
-    // no refill in this evaluation and none pending from an earlier one (each
-    // waited here): the wait would only wait for the wave's row stores
-    if (p.refilled) lds_dma_wait();
-    RWRT_STAMP(12);
+    lds_dma_wait();
     Corners k;
     k.wa = p.wa;
     k.wb = p.wb;
     k.wc = p.wc;
     k.wd = p.wd;
-#ifndef RWRT_LDS_BATCH
-#define RWRT_LDS_BATCH 1
-#endif
-#if RWRT_LDS_BATCH
     double2 v[4][6];   // every read in flight before the first blend
 #pragma unroll
     for (int q = 0; q < 6; ++q)
@@ -680,14 +449,6 @@ struct CachedStaticBG {
       g[2 * q] = blend(k, v[0][q].x, v[1][q].x, v[2][q].x, v[3][q].x);
       if (2 * q + 1 < 11) g[2 * q + 1] = blend(k, v[0][q].y, v[1][q].y, v[2][q].y, v[3][q].y);
     }
-#else
-#pragma unroll
-    for (int q = 0; q < 6; ++q) {
-      const double2 a = chunk(0, q), b = chunk(1, q), c = chunk(2, q), d = chunk(3, q);
-      g[2 * q] = blend(k, a.x, b.x, c.x, d.x);
-      if (2 * q + 1 < 11) g[2 * q + 1] = blend(k, a.y, b.y, c.y, d.y);
-    }
-#endif
   }
   // Only the RHS looks up through the cache: a lane with |lat| > pi/2 is
   // masked there (its l is NaN, so are its derivatives), a NaN lat gives NaN
@@ -705,8 +466,6 @@ __device__ __forceinline__ void lookup_end(const CachedStaticBG& B,
                                            const CachedStaticBG::Pending& p, double g[11]) {
   B.end(p, g);
 }
-
-
 
 template <class T>
 struct VaryingBG {
@@ -1011,15 +770,13 @@ struct LaneBG {
   static constexpr int kLdsBytes = 0;
   __device__ static BG make(const BG& B, char*) { return B; }
 };
-#if RWRT_CELL_CACHE
 template <>
 struct LaneBG<StaticBG> {
   using type = CachedStaticBG;
-  static constexpr int kLdsBytes = 4 * kStaticCacheBytesPerWave;   // 256-thread blocks
+  static constexpr int kLdsBytes = 4 * kCacheBytesPerWave;   // 256-thread blocks
   __device__ static CachedStaticBG make(const StaticBG& B, char* lds) {
     const unsigned wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    return CachedStaticBG{B.F, lds + wave * kStaticCacheBytesPerWave,
-                          (threadIdx.x & 63u) * (RWRT_CACHE_LANE_SLICE ? kSliceStride : 16u), ~0u, ~0u};
+    return CachedStaticBG{B.F, lds + wave * kCacheBytesPerWave, (threadIdx.x & 63u) * 16u, ~0u, ~0u};
   }
 };
 template <>
@@ -1046,10 +803,6 @@ struct LaneBG<VaryingBGA32> {
     return c;
   }
 };
-#ifndef RWRT_CACHE_FP64_LEVELS
-#define RWRT_CACHE_FP64_LEVELS 1
-#endif
-#if RWRT_CACHE_FP64_LEVELS
 template <>
 struct LaneBG<VaryingBG<double>> {
   using type = CachedVaryingBG64;
@@ -1059,45 +812,7 @@ struct LaneBG<VaryingBG<double>> {
     return CachedVaryingBG64{B, lds + wave * kCacheBytesPerWave, (threadIdx.x & 63u) * 16u, ~0u, ~0u, -1};
   }
 };
-#endif
-#endif
 
-// ---------------------------------------------------------------------------
-// sin, cos and tan of one argument with ONE reduction: the ROCm device
-// library's (ocml) f64 algorithms restated operation for operation in
-// rwrt_math.h, so every bit equals sin(), cos() and tan()
-// (tests/test_gpu_parity.py::test_device_math_exactness).  The Horner steps
-// are explicit three-operand v_fma_f64 (the compiler's fmac form copies each
-// hoisted coefficient first: one extra instruction per step).  |x| >= 2^30,
-// inf and NaN take the library routines.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ double fma3(double a, double b, double c) {
-  double d;
-  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
-  return d;
-}
-// ocml's refined reciprocal (v_rcp_f64 + two Newton steps)
-__device__ __forceinline__ double recip2(double b) {
-  double rc = __builtin_amdgcn_rcp(b);
-  rc = fma(fma(-b, rc, 1.0), rc, rc);
-  return fma(fma(-b, rc, 1.0), rc, rc);
-}
-}  // namespace rwrt
-#define RM_FN __device__ __forceinline__
-#define RM_FMA3(a, b, c) ::rwrt::fma3(a, b, c)
-#define RM_RECIP2(b) ::rwrt::recip2(b)
-#include "rwrt_math.h"
-namespace rwrt {
-using rwrt_math::rm_pow;
-__device__ __forceinline__ void sincostan(double x, double& sn, double& cs, double& tn) {
-  if (!(fabs(x) < 0x1p30)) {
-    asm volatile("");   // large, infinite or NaN argument: library routines (rare branch)
-    sincos(x, &sn, &cs);
-    tn = tan(x);
-    return;
-  }
-  rwrt_math::rm_sincostan_small(x, sn, cs, tn);
-}
 }  // namespace rwrt
 
 // ---------------------------------------------------------------------------
@@ -1137,14 +852,7 @@ __device__ __forceinline__ double add_rd(double a, double b) {
 }
 }  // namespace rwrt
 #define NM_FN __device__ __forceinline__
-#ifndef RWRT_NM_CONST_MEM
-#define RWRT_NM_CONST_MEM 0
-#endif
-#if RWRT_NM_CONST_MEM   // (experiment) the polynomial constants as scalar loads, not s_mov pairs
-#define NM_CONST __constant__
-#else
 #define NM_CONST constexpr
-#endif
 #define NM_TABLE constexpr
 #define NM_FMA_RZ(a, b, c) ::rwrt::fma_rz((a), (b), (c))
 #define NM_MUL_RZ(a, b) ::rwrt::mul_rz((a), (b))
@@ -1159,12 +867,6 @@ __device__ __forceinline__ double add_rd(double a, double b) {
 // nm_stage): per-lane table reads from global memory would share vmcnt with
 // the cell cache's LDS-DMA refills, so every read would also wait for the
 // refill the RHS issued before its trigonometry.
-#ifndef RWRT_NM_LDS
-#define RWRT_NM_LDS 1
-#endif
-#if RWRT_DIAG_NM_TAB0    // timing-only diagnostic build: every table read at a lane-uniform index
-#define NM_LD(t, i) (t)[(i) & 0]
-#elif RWRT_NM_LDS
 __shared__ unsigned long long nm_lds_kG_SINCOSTAB[440];
 __shared__ unsigned long long nm_lds_kT_TAN_HI[16];
 __shared__ unsigned long long nm_lds_kT_TAN_LO[16];
@@ -1174,103 +876,19 @@ __shared__ unsigned long long nm_lds_kP_EXP_HI[16];
 __shared__ unsigned long long nm_lds_kP_EXP_LO[16];
 __shared__ unsigned nm_lds_kRCP14_KNOT[128];
 #define NM_LD(t, i) nm_lds_##t[i]
-#endif
-// The NumPy-math polynomial and reduction constants from LDS
-// (RWRT_NM_KLDS): a compile-time constant operand of the math costs one
-// ds_read_b64 issue slot instead of an s_mov_b32 pair rebuilt at each use
-// (SGPR pressure makes the compiler rematerialise them).
-#ifndef RWRT_NM_KLDS
-#define RWRT_NM_KLDS 0
-#endif
-#if RWRT_NM_KLDS && RWRT_NM_LDS && !RWRT_DIAG_NM_TAB0
-#include "np_math_tables.h"
-#define NM_KLIST(X) \
-  X(kG_HP0) \
-  X(kG_HP1) \
-  X(kG_MHP1) \
-  X(kG_T126) \
-  X(kG_S5) \
-  X(kG_S4) \
-  X(kG_S3) \
-  X(kG_S2) \
-  X(kG_S1) \
-  X(kG_BIG) \
-  X(kG_SN5) \
-  X(kG_SN3) \
-  X(kG_CS6) \
-  X(kG_CS4) \
-  X(kG_CS2) \
-  X(kG_TOINT) \
-  X(kG_HPINV) \
-  X(kG_MP1) \
-  X(kG_MP2) \
-  X(kG_PP3) \
-  X(kG_PP4) \
-  X(kT_INVPI16) \
-  X(kT_PI16A) \
-  X(kT_PI16B) \
-  X(kT_PI16C) \
-  X(kT_C1) \
-  X(kT_C2) \
-  X(kT_C3) \
-  X(kT_C4) \
-  X(kT_C5) \
-  X(kT_ONE) \
-  X(kT_SHIFT) \
-  X(kT_BIGARG) \
-  X(kP_HALF) \
-  X(kP_C1) \
-  X(kP_C10) \
-  X(kP_C9) \
-  X(kP_C8) \
-  X(kP_C7) \
-  X(kP_C6) \
-  X(kP_C5) \
-  X(kP_C4) \
-  X(kP_C3) \
-  X(kP_LN) \
-  X(kP_LP) \
-  X(kP_E7) \
-  X(kP_E6) \
-  X(kP_E4) \
-  X(kP_E3) \
-  X(kP_E2) \
-  X(kP_E1) \
-  X(kP_TOVF)
-enum NmKIdx {
-#define NM_KENUM(name) NM_KIDX_##name,
-  NM_KLIST(NM_KENUM)
-#undef NM_KENUM
-  NM_KCOUNT
-};
-__constant__ unsigned long long nm_kvals[NM_KCOUNT] = {
-#define NM_KVALS(name) np_math::name,
-    NM_KLIST(NM_KVALS)
-#undef NM_KVALS
-};
-__shared__ double nm_lds_k[NM_KCOUNT];
-__device__ __forceinline__ double nm_kval(unsigned long long u) {
-  if (__builtin_constant_p(u)) {
-#define NM_KTRY(name) \
-  if (u == np_math::name) return nm_lds_k[NM_KIDX_##name];
-    NM_KLIST(NM_KTRY)
-#undef NM_KTRY
-  }
-  return __builtin_bit_cast(double, u);
-}
-#define NM_KVAL(u) nm_kval(u)
-#endif
+// (The polynomial constants stay s_mov_b32 pairs: as scalar loads they share
+// lgkmcnt with the LDS reads, 0.99x; from LDS the round trip lands on the
+// polynomial chains, 0.91x -- profiles/r2/ab/const_lds.txt.)
 #include "np_math.h"
 
 namespace rwrt {
 // Copies the tables a kernel's math reads into its LDS (every thread of the
 // block must call it, before any other use): NM_SINCOS = glibc's sin/cos
 // table, NM_TAN = SVML tan's tables, NM_POW = SVML pow's (both with the
-// VRCP14 knots).  A no-op when the tables are read from global memory.
+// VRCP14 knots).
 enum { NM_SINCOS = 1, NM_TAN = 2, NM_POW = 4, NM_ALL = 7 };
 template <int MASK>
 __device__ __forceinline__ void nm_stage() {
-#if RWRT_NM_LDS && !RWRT_DIAG_NM_TAB0
   const int t = threadIdx.x, nt = blockDim.x;
   if (MASK & NM_SINCOS)
     for (int i = t; i < 440; i += nt) nm_lds_kG_SINCOSTAB[i] = np_math::kG_SINCOSTAB[i];
@@ -1290,67 +908,25 @@ __device__ __forceinline__ void nm_stage() {
     }
   if (MASK & (NM_TAN | NM_POW))
     for (int i = t; i < 128; i += nt) nm_lds_kRCP14_KNOT[i] = np_math::kRCP14_KNOT[i];
-#if RWRT_NM_KLDS
-  for (int i = t; i < NM_KCOUNT; i += nt) nm_lds_k[i] = __builtin_bit_cast(double, nm_kvals[i]);
-#endif
   __syncthreads();
-#endif
 }
 
-// The kernels' transcendentals: the reference NumPy's (default) or, in the
-// RWRT_MATH_NUMPY=0 diagnostic build, the device library's algorithms
-// (rwrt_math.h; last-bit different from the reference).
-#ifndef RWRT_MATH_NUMPY
-#define RWRT_MATH_NUMPY 1
-#endif
+// The kernels' transcendentals: the reference NumPy's.
 __device__ __forceinline__ double k_sin(double x) {
-#if RWRT_MATH_NUMPY
   return np_math::nm_sin(x);
-#else
-  double s, c, t;
-  sincostan(x, s, c, t);
-  return s;
-#endif
 }
 __device__ __forceinline__ double k_cos(double x) {
-#if RWRT_MATH_NUMPY
   return np_math::nm_cos(x);
-#else
-  double s, c, t;
-  sincostan(x, s, c, t);
-  return c;
-#endif
 }
 __device__ __forceinline__ double k_tan(double x) {
-#if RWRT_MATH_NUMPY
   return np_math::nm_tan(x);
-#else
-  double s, c, t;
-  sincostan(x, s, c, t);
-  return t;
-#endif
 }
-#ifndef RWRT_POW_NUMPY
-#define RWRT_POW_NUMPY RWRT_MATH_NUMPY
-#endif
 __device__ __forceinline__ double k_pow(double x, double y) {
-#if RWRT_POW_NUMPY
   return np_math::nm_pow(x, y);
-#else
-  return rm_pow(x, y);
-#endif
 }
 // sin, cos, tan of a latitude (the RHS): the same values as k_sin/k_cos/k_tan
 __device__ __forceinline__ void k_sincostan(double x, double& s, double& c, double& t) {
-#if RWRT_MATH_NUMPY
   np_math::nm_sincostan(x, s, c, t);
-#elif RWRT_RHS_TRIG_SMALL
-  // |lat| >= 2^30, inf or NaN: the ray is masked (|lat| >= pi/2) or its
-  // lookup is NaN, so every output is NaN whatever s, c, tn are
-  rwrt_math::rm_sincostan_small(x, s, c, t);
-#else
-  sincostan(x, s, c, t);
-#endif
 }
 
 // Mercator factors of cal_bs_mercator_point (bs.py:856-860).
@@ -1417,7 +993,7 @@ struct KapTerms {
 };
 __device__ __forceinline__ KapTerms kap_terms(double k, double l) {
   KapTerms w;
-  w.kap = RDIV(l, k);
+  w.kap = l / k;
   w.kap2 = w.kap * w.kap;
   w.kap1 = 1.0 + w.kap2;
   w.kk = (k * k) * w.kap1;
@@ -1446,9 +1022,6 @@ __device__ __forceinline__ void ugvg(double fu, double fv, double fqx, double fq
 // aux (optional) receives {ug, vg, cos(lat)} of this evaluation -- exactly what
 // the per-interval post-processing recomputes at the same position
 // (wr.py:844, 856-865) -- or NaN for a masked ray (no values computed).
-#ifndef RWRT_KAP_EARLY
-#define RWRT_KAP_EARLY 1
-#endif
 template <class BG>
 __device__ __forceinline__ void ray_rhs(const BG& B, double t, const double* y, double* dy,
                                         double* aux = nullptr) {
@@ -1459,49 +1032,21 @@ __device__ __forceinline__ void ray_rhs(const BG& B, double t, const double* y, 
   const bool bad = fabs(lat) >= kHalfPi || fabs(y[3]) >= 100.0;
   const double ky = bad ? kNaN : y[3], amp = y[4];
   double g[11];
-  RWRT_STAMP(0);
-#if RWRT_TRIG_EARLY && RWRT_MATH_NUMPY && !RWRT_DIAG_NOTRIG
   // the trigonometry's table reads and tan polynomial beside the lookup's cell
   // arithmetic (one scheduling region: the refill below is a branch)
   const auto trig = np_math::nm_sincostan_begin(lat);
-#endif
   double s, c;
-#if RWRT_KAP_EARLY
   const KapTerms kw = kap_terms(kx, ky);   // (k, l only: beside the trig and the cell arithmetic)
-#endif
-#if !RWRT_DIAG_NOINTERP
   const auto pending = lookup_begin(B, lon, lat, t);   // the lookup's fill overlaps the trig
-#endif
-  RWRT_STAMP(1);
-#if RWRT_DIAG_NOTRIG     // timing-only diagnostic build: polynomial stand-ins
-  s = lat * (1.0 - lat * lat * (1.0 / 6.0));
-  c = 1.0 - lat * lat * 0.5;
-  const double tn = lat * (1.0 + lat * lat * (1.0 / 3.0));
-#elif RWRT_TRIG_EARLY && RWRT_MATH_NUMPY
   double tn;
   np_math::nm_sincostan_end(lat, trig, s, c, tn);   // == k_sincostan(lat, s, c, tn)
-#else
-  double tn;
-  k_sincostan(lat, s, c, tn);       // np.cos, np.sin, np.tan of lat (bs.py:856-880)
-#endif
-  RWRT_STAMP(2);
-#if RWRT_DIAG_NOINTERP   // timing-only diagnostic build: constant background
-#pragma unroll
-  for (int q = 0; q < 11; ++q) g[q] = 1e-5 * (q + 1) + 1e-9 * lat;
-#else
   __builtin_amdgcn_sched_barrier(0);
   lookup_end(B, pending, g);
-#endif
-  RWRT_STAMP(3);
   const Merc M = merc_factors(lat, c, s);
   double o[12];
   mercator12(g, M, tn, o);
-  RWRT_STAMP(4);
   const double fmu = o[0], fmv = o[1], fmux = o[2], fmuy = o[3], fmvx = o[4], fmvy = o[5];
   const double fmqx = o[6], fmqy = o[7], fmqxx = o[8], fmqxy = o[9], fmqyx = o[10], fmqyy = o[11];
-#if !RWRT_KAP_EARLY
-  const KapTerms kw = kap_terms(kx, ky);
-#endif
   double ug, vg;
   ugvg(fmu, fmv, fmqx, fmqy, kw, ug, vg);
   // core_diffun (wr.py:53-78); freq only feeds the dead ps/up terms
@@ -1518,7 +1063,6 @@ __device__ __forceinline__ void ray_rhs(const BG& B, double t, const double* y, 
   div2(ug, kREarth, vg * c, kREarth, dy[0], dy[1]);     // x / R, x / R
   div2(dzwn, kREarth, dmwn, kREarth, dy[2], dy[3]);
   dy[4] = div_rearth(damp * amp);
-  RWRT_STAMP(5);
   if (aux) {
     aux[0] = ug;
     aux[1] = vg;
@@ -1641,54 +1185,16 @@ __device__ __forceinline__ double cal_dis_c(double lon_c, double lat_c, double l
 // sin() of two arguments through the one-reduction routine (== sin() for
 // |x| < 2^30), with one shared fallback branch to the library for the rest
 __device__ __forceinline__ void sin2(double a, double b, double& sa, double& sb) {
-#if RWRT_MATH_NUMPY
   sa = k_sin(a);
   sb = k_sin(b);
-#else
-  double c, t;
-  rwrt_math::rm_sincostan_small(a, sa, c, t);
-  rwrt_math::rm_sincostan_small(b, sb, c, t);
-  if (!(fabs(a) < 0x1p30 && fabs(b) < 0x1p30)) {
-    asm volatile("");   // huge, infinite or NaN: library routines (rare branch)
-    sa = sin(a);
-    sb = sin(b);
-  }
-#endif
 }
 // cos() of an argument known to be below pi/2 in magnitude or NaN
 __device__ __forceinline__ double cos_small(double x) {
-#if RWRT_MATH_NUMPY
   return k_cos(x);
-#else
-  double sn, cs, tn;
-  rwrt_math::rm_sincostan_small(x, sn, cs, tn);
-  return cs;
-#endif
 }
-#ifndef RWRT_JUMP_FAST_SIN
-#define RWRT_JUMP_FAST_SIN 0   // measured -1.3 % on C3 (profiles/r2/ab/stage_partial.txt)
-#endif
 __device__ __forceinline__ bool cal_dis_reaches(double lon_c, double lat_c, double lon_p,
                                                 double lat_p, double cos_c, double cos_p,
                                                 double cut_off, double cut_a) {
-#if RWRT_JUMP_FAST_SIN && RWRT_MATH_NUMPY
-  // The "certainly no jump" verdict only needs a within ~1e-15 relative of the
-  // reference's (the margin of cut_a is 1e-9): the device library's sines
-  // (<= 2 ulp) decide it; the reference NumPy's own sines are evaluated only
-  // for the exact comparison near the threshold.
-  const double dlat2 = (lat_c - lat_p) / 2.0, dlon2 = (lon_c - lon_p) / 2.0;
-  const double fd = ::sin(dlat2), fl = ::sin(dlon2);
-  const double af = fd * fd + (cos_p * cos_c) * (fl * fl);
-  bool r = false;
-  if (!(af < cut_a)) {
-    asm volatile("");   // rare: near or past the threshold, or NaN
-    double sd, sl;
-    sin2(dlat2, dlon2, sd, sl);
-    const double a = sd * sd + (cos_p * cos_c) * (sl * sl);
-    r = fabs(2.0 * atan2(sqrt(a), sqrt(1.0 - a))) >= cut_off;
-  }
-  return r;
-#else
   double sd, sl;
   sin2((lat_c - lat_p) / 2.0, (lon_c - lon_p) / 2.0, sd, sl);
   const double a = sd * sd + (cos_p * cos_c) * (sl * sl);
@@ -1698,7 +1204,6 @@ __device__ __forceinline__ bool cal_dis_reaches(double lon_c, double lat_c, doub
     r = fabs(2.0 * atan2(sqrt(a), sqrt(1.0 - a))) >= cut_off;
   }
   return r;
-#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -1828,18 +1333,12 @@ __device__ __forceinline__ double stage_input(const KS& K, double t, const doubl
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
     ys[v] = y[v] + wsum<S, NV>(K, f, v) * h;
-#if RWRT_STAGE_BARRIER
-    __builtin_amdgcn_sched_barrier(0);   // bound the LDS reads in flight (registers)
-#endif
   }
   return t + kCs[S] * h;
 }
 
 // The first J terms of wsum<S> (J < S) for every variable, in wsum's order
 // (more than one variable: sequential in j).
-#ifndef RWRT_STAGE_PARTIAL
-#define RWRT_STAGE_PARTIAL 1
-#endif
 template <int S, int J, int NV, class KS>
 __device__ __forceinline__ void stage_part(const KS& K, const double* f, double* part) {
 #pragma unroll
@@ -1862,17 +1361,10 @@ __device__ __forceinline__ void error_part(const KS& K, const double* f, double*
   }
 }
 
-// A problem whose RHS is evaluated by a whole block (rk45_team_kernel) says so
-// with kTeam = true and a stage(s, t, y, dy) member.
-template <class P, class = void>
-struct IsTeam : std::false_type {};
-template <class P>
-struct IsTeam<P, std::void_t<decltype(P::kTeam)>> : std::bool_constant<P::kTeam> {};
-
 // One DP5(4) attempt: rk_step (rkf45.py:259-321) + _estimate_error_norm
 // (rkf45.py:368-373).  The six stage evaluations are unrolled (six inlined RHS
-// copies, ~45 KB of code: fits the instruction cache; RWRT_UNROLL_STAGES=0
-// keeps one copy in a wave-uniform stage loop).  Returns the error norm (NaN kept); fills y_new,
+// copies: fits the instruction cache; one copy in a wave-uniform stage loop
+// measured 0.92x).  Returns the error norm (NaN kept); fills y_new,
 // K6, if aux is given the problem's side outputs of the K6 evaluation (at
 // y_new), and if Kout is given all seven stages.
 template <class P, class KS>
@@ -1883,10 +1375,6 @@ __device__ __forceinline__ double dp54_attempt(const P& fun, KS& K, double t, co
                                                double* aux = nullptr) {
   constexpr int NV = P::NV;
   double ys[NV], r[NV];
-#ifndef RWRT_UNROLL_STAGES
-#define RWRT_UNROLL_STAGES 1   // six inlined RHS copies: no stage dispatch (the code fits the I-cache)
-#endif
-#if RWRT_STAGE_PARTIAL
   if constexpr (NV > 1) {
     // Each stage's weighted sum is sequential in j and its newest stage comes
     // last: the terms of the older stages are summed while the current RHS
@@ -1897,11 +1385,7 @@ __device__ __forceinline__ double dp54_attempt(const P& fun, KS& K, double t, co
 #pragma unroll
     for (int v = 0; v < NV; ++v) ys[v] = y[v] + wsum<1, NV>(K, f, v) * h;
     double ts = t + kCs[1] * h;
-#if RWRT_UNROLL_STAGES
 #pragma unroll
-#else
-#pragma nounroll
-#endif
     for (int s = 1; s <= 6; ++s) {
       double w = 0.0, cn = 0.0;   // the newest term's weight and the time offset of stage s + 1
       switch (s) {   // wave-uniform (compile-time when unrolled)
@@ -1912,8 +1396,7 @@ __device__ __forceinline__ double dp54_attempt(const P& fun, KS& K, double t, co
         case 5: stage_part<6, 5, NV>(K, f, part); w = kW[6][5]; cn = kCs[6]; break;
         default: error_part<NV>(K, f, part); break;
       }
-      if constexpr (IsTeam<P>::value) fun.stage(s, ts, ys, r);
-      else fun(ts, ys, r, aux);
+      fun(ts, ys, r, aux);
       if (s < 6) {
         K.put_stage(s, r);
 #pragma unroll
@@ -1931,7 +1414,6 @@ __device__ __forceinline__ double dp54_attempt(const P& fun, KS& K, double t, co
       const double x = e / sc;
       ss = (v == 0) ? x * x : ss + x * x;
     }
-    RWRT_STAMP(6);
     if (Kout) {
 #pragma unroll
       for (int j = 0; j < 6; ++j)
@@ -1942,12 +1424,8 @@ __device__ __forceinline__ double dp54_attempt(const P& fun, KS& K, double t, co
     }
     return sqrt(ss) / RootN<NV>::v;
   }
-#endif
-#if RWRT_UNROLL_STAGES
+  // one variable (the stepper KATs): einsum's even/odd sums (wsum)
 #pragma unroll
-#else
-#pragma nounroll
-#endif
   for (int s = 1; s <= 6; ++s) {
     double ts;
     switch (s) {   // wave-uniform: one straight-line combination per stage
@@ -1958,8 +1436,7 @@ __device__ __forceinline__ double dp54_attempt(const P& fun, KS& K, double t, co
       case 5: ts = stage_input<5, NV>(K, t, y, f, h, ys); break;
       default: ts = stage_input<6, NV>(K, t, y, f, h, ys); break;
     }
-    if constexpr (IsTeam<P>::value) fun.stage(s, ts, ys, r);   // the block's four waves together
-    else fun(ts, ys, r, aux);
+    fun(ts, ys, r, aux);
     if (s < 6) K.put_stage(s, r);
   }
   // after the loop: ys = y + h*(B . K[:6]) = y_new, r = K6
@@ -1990,7 +1467,6 @@ __device__ __forceinline__ double dp54_attempt(const P& fun, KS& K, double t, co
     const double x = e / sc;
     ss = (v == 0) ? x * x : ss + x * x;
   }
-  RWRT_STAMP(6);
   if (Kout) {
 #pragma unroll
     for (int j = 0; j < 6; ++j)
@@ -2083,14 +1559,10 @@ struct Lane {
     double en = dp54_attempt(fun, K, t, y, f, h, rtol, atol, yn, k6, nullptr, 0,
                              P::NAUX > 0 ? aux : nullptr);
     if (en != en) en = 0.0;                 // rkf45.py:446
-#if RWRT_DIAG_NOPOW
-    const double sp = kSafety / (0.5 + en);
-#else
     // SAFETY * error_norm ** (-1/5), shared by the accept (rkf45.py:453-469) and
     // reject (rkf45.py:471-475) factors: one pow per attempt even when the
     // wave's lanes split between the two outcomes
     const double sp = kSafety * k_pow(en, kErrExp);
-#endif
     // Accept / reject as selects: the lanes of a wave usually disagree, and
     // a branch pair would execute both sides anyway.
     const bool acc = en < 1.0;
@@ -2110,7 +1582,6 @@ struct Lane {
     rejected = rejected || !acc;
     nacc += acc ? 1 : 0;
     nrej += acc ? 0 : 1;
-    RWRT_STAMP(7);
     return (acc && t - tb >= 0.0) ? kReached : kStep;   // rkf45.py:250
   }
 };
@@ -2237,7 +1708,7 @@ struct RunArgs {
   int32_t* nanrow;
   double* out;
   int32_t* queue;       // [1]: the work queue's head ([0] unused)
-  int64_t n_heavy;      // order[0, n_heavy): rays of rk45_team_kernel (latency mode); the queue is the rest
+  int64_t n_heavy;      // order[0, n_heavy): rays in latency mode (quad_rays); the queue is the rest
   int32_t heavy_blocks; // blocks [0, heavy_blocks) run order[0, n_heavy) in latency mode (quad_rays)
   double cut_a;         // haversine argument certainly below cut_off (cal_dis_below)
   const uint8_t* frozen;  // rays frozen at the launch start (NULL: none skipped), see frozen_fill_kernel
@@ -2279,9 +1750,6 @@ inline double haversine_cut(double cut_off) {
 // heavy rays also diverges less often (interval ends, cell refills) than one
 // of 64.
 // ---------------------------------------------------------------------------
-#ifndef RWRT_LATENCY_QUAD
-#define RWRT_LATENCY_QUAD 1   // n_heavy rays run in quad_rays (0: rk45_team_kernel)
-#endif
 
 // x of lane (quad base + P[role]) for every lane of the quad (DPP quad_perm;
 // every lane of a quad is active whenever one is: they share the ray)
@@ -2308,13 +1776,10 @@ struct QuadRole {
 // records r and r + 4, roles 2 and 3 record r only: u v qxx qxy | ux uy qyy |
 // vx vy | qx qy), 8 LDS reads per lane instead of 24, then broadcast; each
 // field is the same blend of the same corner values (bit for bit).
-#ifndef RWRT_QUAD_BLEND_SPLIT
-#define RWRT_QUAD_BLEND_SPLIT 1
-#endif
 __device__ __forceinline__ void quad_lookup_end(const CachedStaticBG& B, const QuadRole& R,
                                                 const CachedStaticBG::Pending& p, double g[11]) {
-  static_assert(!RWRT_CACHE_LANE_SLICE, "quad_lookup_end reads the chunk-major slice layout");
-  if (p.refilled) lds_dma_wait();
+  static_assert(!0, "quad_lookup_end reads the chunk-major slice layout");
+  lds_dma_wait();
   Corners k;
   k.wa = p.wa;
   k.wb = p.wb;
@@ -2359,11 +1824,7 @@ __device__ __forceinline__ void quad_rhs(const CachedStaticBG& B, const QuadRole
   double s, c, tn;
   np_math::nm_sincostan_end(lat, trig, s, c, tn);
   __builtin_amdgcn_sched_barrier(0);
-#if RWRT_QUAD_BLEND_SPLIT
   quad_lookup_end(B, R, pending, g);
-#else
-  lookup_end(B, pending, g);
-#endif
   // Mercator (bs.py:856-883): M.cp == c off the pole band; there every
   // output takes mercator12_masked's extra factor m
   const Merc M = merc_factors(lat, c, s);
@@ -2512,7 +1973,6 @@ __device__ __forceinline__ double quad_attempt(const CachedStaticBG& B, const Qu
 __device__ __forceinline__ bool quad_dis_reaches(const QuadRole& R, double lon_c, double lat_c,
                                                  double lon_p, double lat_p, double cos_c,
                                                  double cos_p, double cut_off, double cut_a) {
-#if RWRT_MATH_NUMPY
   const double dlat2 = (lat_c - lat_p) / 2.0, dlon2 = (lon_c - lon_p) / 2.0;
   const double sv = k_sin(R.odd ? dlon2 : dlat2);
   const double sd = qbcast<0>(sv), sl = qbcast<1>(sv);
@@ -2523,9 +1983,6 @@ __device__ __forceinline__ bool quad_dis_reaches(const QuadRole& R, double lon_c
     r = fabs(2.0 * atan2(sqrt(a), sqrt(1.0 - a))) >= cut_off;
   }
   return r;
-#else
-  return cal_dis_reaches(lon_c, lat_c, lon_p, lat_p, cos_c, cos_p, cut_off, cut_a);
-#endif
 }
 
 // Rows [it_begin, it_end) of rays order[0, n_heavy), one per quad (64 per
@@ -2673,62 +2130,34 @@ __device__ __forceinline__ void quad_rays(const RunArgs<StaticBG>& a, char* cach
 //
 // Load balance: the work per ray per chunk spans 15x the mean (C3); the
 // slowest rays set the makespan.  The host orders rays by the work they did in
-// the previous chunk (longest first) and may hand the heaviest ones to
-// rk45_team_kernel (latency mode, order[0, n_heavy)); this kernel's queue is
-// the rest.
-#ifndef RWRT_WAVES_PER_SIMD
-#define RWRT_WAVES_PER_SIMD 1
-#endif
-#ifndef RWRT_RUN_PRIO
-#define RWRT_RUN_PRIO 1
-#endif
-#ifndef RWRT_DIAG_NOSTORE
-#define RWRT_DIAG_NOSTORE 0
-#endif
-#ifndef RWRT_DIAG_NOFROZENFILL   // timing-only diagnostic build: frozen rays write one row
-#define RWRT_DIAG_NOFROZENFILL 0
-#endif
-#ifndef RWRT_K_IN_LDS
-#define RWRT_K_IN_LDS 1   // stages in LDS: frees 60 VGPRs (in registers they spill to scratch)
-#endif
-#if RWRT_K_IN_LDS
+// the previous chunk (longest first) and may hand the heaviest ones to the
+// latency mode (quad_rays in the grid's first blocks, order[0, n_heavy)); the
+// queue is the rest.
 using KStore = KShared<5>;
-#else
-using KStore = KRegs<5>;
-#endif
 template <class BG>
-__global__ void __launch_bounds__(256, RWRT_WAVES_PER_SIMD) rk45_run_kernel(RunArgs<BG> a) {
+__global__ void __launch_bounds__(256, 1) rk45_run_kernel(RunArgs<BG> a) {
   nm_stage<NM_ALL>();
   using LBG = typename LaneBG<BG>::type;
   using RayProblem = RayProblemT<LBG>;
   // all LDS in one array: the stages (5 x 5 doubles per lane) then the lookup cache
   constexpr int kKBytes = 5 * 5 * 256 * 8;
   __shared__ __attribute__((aligned(16))) char smem[kKBytes + LaneBG<BG>::kLdsBytes];
-#if RWRT_LATENCY_QUAD
   if constexpr (std::is_same<BG, StaticBG>::value) {
     if ((int)blockIdx.x < a.heavy_blocks) {   // (block-uniform) latency mode
-      if (RWRT_RUN_PRIO) __builtin_amdgcn_s_setprio(1);
+      if (1) __builtin_amdgcn_s_setprio(1);
       quad_rays(a, smem + kKBytes, reinterpret_cast<double*>(smem));
       return;
     }
   }
-#endif
   const RayProblem P{LaneBG<BG>::make(a.B, smem + kKBytes)};
   const int64_t nrows = a.it_end - a.it_begin;
-#if RWRT_DIAG_STAMPS
-  stamp_init();
-#endif
-#if RWRT_K_IN_LDS
   Lane<RayProblem, KStore> L;
   L.K.p = reinterpret_cast<double*>(smem) + threadIdx.x;
   L.K.stride = 256;
-#else
-  Lane<RayProblem, KStore> L;
-#endif
   int64_t ray = -1, nacc = 0, nrej = 0;
   int32_t it = 0, nanrow = 0;
   double prev_lon = 0.0, prev_lat = 0.0, cos_prev = 0.0;
-  if (RWRT_RUN_PRIO) {
+  if (1) {
     // above frozen_fill_kernel's waves (priority 0) sharing the SIMD: the
     // fill takes the issue cycles the ray loop leaves idle
     __builtin_amdgcn_s_setprio(1);
@@ -2761,14 +2190,9 @@ __global__ void __launch_bounds__(256, RWRT_WAVES_PER_SIMD) rk45_run_kernel(RunA
       cos_prev = k_cos(prev_lat);
       L.aux[2] = kNaN;     // no evaluation at y yet
     }
-#if RWRT_DIAG_TB_ARITH   // timing-only diagnostic build: t_bound = it * 2 h (the bench's schedule), no load
-    const double tb = (double)it * 7200.0;
-#else
     const double tb = a.tbound[it];
-#endif
     const int st = L.iterate(P, tb, a.min_step, a.rtol, a.atol, nacc, nrej);
     if (st == Lane<RayProblem, KStore>::kStep) continue;
-    RWRT_STAMP(8);
 
     // ---- interval it reached: post-processing (wr.py:835-885) ----
     // The last accepted step's K6 evaluation was at this y: its cos(lat), ug
@@ -2783,11 +2207,7 @@ __global__ void __launch_bounds__(256, RWRT_WAVES_PER_SIMD) rk45_run_kernel(RunA
     bool masked = fabs(y[1]) >= kHalfPi;
     if (!masked) {
       cos_c = have ? L.aux[2] : cos_small(y[1]);   // |y[1]| < pi/2 or NaN here
-#if RWRT_DIAG_NOPOST
-      masked = fabs(y[1] - prev_lat) >= a.cut_off;
-#else
       masked = cal_dis_reaches(y[0], y[1], prev_lon, prev_lat, cos_c, cos_prev, a.cut_off, a.cut_a);
-#endif
     }
     if (masked) {
 #pragma unroll
@@ -2807,14 +2227,14 @@ __global__ void __launch_bounds__(256, RWRT_WAVES_PER_SIMD) rk45_run_kernel(RunA
     // masks against itself is a no-op), so every remaining row of the chunk
     // equals this one: write them all and release the lane.
     const int last = (st == Lane<RayProblem, KStore>::kFrozen) ? a.it_end : it + 1;
-    if (!RWRT_DIAG_NOSTORE) {   // (timing-only diagnostic build: no row stores)
+    if (!0) {   // (timing-only diagnostic build: no row stores)
       double2* o = reinterpret_cast<double2*>(a.out + ((size_t)ray * nrows + (it - a.it_begin)) * RWRT_NOUT);
-      store_row16<RWRT_NT_ROWS>(o + 0, r0);
-      store_row16<RWRT_NT_ROWS>(o + 1, r1);
-      store_row16<RWRT_NT_ROWS>(o + 2, r2);
-      store_row16<RWRT_NT_ROWS>(o + 3, r3);
+      store_row16<0>(o + 0, r0);
+      store_row16<0>(o + 1, r1);
+      store_row16<0>(o + 2, r2);
+      store_row16<0>(o + 3, r3);
     }
-    if (!RWRT_DIAG_NOFROZENFILL && last > it + 1) {
+    if (!0 && last > it + 1) {
       asm volatile("");   // frozen: the remaining rows of the chunk (rare branch)
       for (int k = it + 1; k < last; ++k) {
         double2* o = reinterpret_cast<double2*>(a.out + ((size_t)ray * nrows + (k - a.it_begin)) * RWRT_NOUT);
@@ -2825,7 +2245,6 @@ __global__ void __launch_bounds__(256, RWRT_WAVES_PER_SIMD) rk45_run_kernel(RunA
       }
     }
     if (nanrow == a.nt && isnan(y[0])) nanrow = it;  // wr.py:853-855 (host reduces)
-    RWRT_STAMP(9);
     prev_lon = y[0];
     prev_lat = y[1];
     cos_prev = cos_c;
@@ -2845,9 +2264,6 @@ __global__ void __launch_bounds__(256, RWRT_WAVES_PER_SIMD) rk45_run_kernel(RunA
       ray = -1;
     }
   }
-#if RWRT_DIAG_STAMPS
-  stamp_flush();
-#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -2878,12 +2294,6 @@ __global__ void frozen_flag_kernel(const double* __restrict__ state, int64_t nra
 // KB sin/cos table, one wave per block) beside the run kernel's 155 KB, or
 // the fill would wait for the run to end.
 constexpr int kFillThreads = 64;
-#ifndef RWRT_FILL_THROTTLE
-#define RWRT_FILL_THROTTLE 64
-#endif
-#ifndef RWRT_FILL_SLEEP      // s_sleep units (64 clocks) per RWRT_FILL_THROTTLE rows
-#define RWRT_FILL_SLEEP 32
-#endif
 // Every row of a launch for each frozen ray of a fill tile (one wave, ray
 // base + lane): one ray's rows at a time, 16 B per thread, contiguous (a
 // ray's rows are); thread t stores quarter t & 3 of the 64-B row, read from
@@ -2904,13 +2314,11 @@ __device__ __forceinline__ void write_frozen_tile(double* out, int64_t base, int
     const double2 q2 = make_double2(__shfl(r2.x, j), __shfl(r2.y, j));
     const double2 q3 = make_double2(__shfl(r3.x, j), __shfl(r3.y, j));
     const double2 v = qt == 0 ? q0 : qt == 1 ? q1 : qt == 2 ? q2 : q3;
-    for (int64_t q = threadIdx.x; q < nq; q += kFillThreads) store_row16<RWRT_NT_FILL>(o + q, v);
-#if RWRT_FILL_THROTTLE
+    for (int64_t q = threadIdx.x; q < nq; q += kFillThreads) store_row16<1>(o + q, v);
     // pace the stores (~0.9 us per full 64 rows written; none for shorter
     // chunks): a full-rate fill floods the memory queues the run kernel's
     // lookups wait in
-    for (int64_t z = RWRT_FILL_THROTTLE; z <= nrows; z += RWRT_FILL_THROTTLE) __builtin_amdgcn_s_sleep(RWRT_FILL_SLEEP);
-#endif
+    for (int64_t z = 64; z <= nrows; z += 64) __builtin_amdgcn_s_sleep(32);
   }
 }
 
@@ -2960,268 +2368,6 @@ frozen_fill_kernel(RunArgs<BG> a) {
   write_frozen_tile(a.out, base, nrows, mine, r0, r1, r2, r3);
 }
 
-// ---------------------------------------------------------------------------
-// Latency mode: rk45_team_kernel.  One ray per lane as in rk45_run_kernel, but
-// each RHS evaluation of a ray is split over the four waves of its block --
-// one per SIMD -- so that the independent pieces of wr.py:492-556 run side by
-// side instead of one after another on one SIMD:
-//
-//   phase 1  wave 0: the bilinear lookup (cell cache)  wave 1: sin, cos of lat
-//            wave 2: tan of lat                        (bs.py:781-887)
-//   phase 2  wave 0: fu/cos, fv/cos   wave 1: ux/cos, vx/cos   (bs.py:862-883)
-//            wave 2: cal_ugvg's two quotients (wn.py:266-294)
-//            wave 3: core_diffun's qk, ql and damp2 (wr.py:53-78)
-//   phase 3  wave 0: damp1 -> damp -> dy4   wave 1: dy0, dy1   wave 2: dy2, dy3
-//
-// exchanging values through LDS between the phases (three barriers per RHS).
-// Everything else -- stage inputs, step control, pow, the interval masks -- is
-// computed by all four waves on identical values, so their control flow (and
-// with it every barrier) stays the same; wave 0 alone writes to memory.  Each
-// value is the same operation on the same operands as in ray_rhs, so the
-// results are the run kernel's bit for bit (tests/test_gpu_team.py).  A ray's
-// attempt then costs roughly the longest phase chain instead of the whole
-// instruction stream: the tail of a launch (the heaviest rays, C3/C4) runs
-// ~2-3x faster, at a quarter of the rays per SIMD.
-// ---------------------------------------------------------------------------
-enum TeamSlot {
-  TX_G = 0,                          // g[11] (phase 1, wave 0)
-  TX_S = 11, TX_C, TX_TN,            // sin, cos, tan of lat (waves 1, 2)
-  TX_DU, TX_DV, TX_DUX, TX_DVX,      // the four Mercator quotients (waves 0, 1)
-  TX_QU, TX_QV,                      // cal_ugvg's quotients (wave 2)
-  TX_QK, TX_QL, TX_DAMP2,            // core_diffun's (wave 3)
-  kTeamSlots
-};
-constexpr int kTeamLanes = 64;
-
-// K1..K6 of the block's rays in LDS, [stage][variable][lane]: written by the
-// RHS's phase 3, read by every wave (K0 is the step's f, in registers)
-struct KTeam {
-  double* p;   // this lane's column
-  __device__ __forceinline__ double get(int j, int v) const { return p[(j * 5 + v) * kTeamLanes]; }
-  __device__ __forceinline__ void put_stage(int, const double*) {}
-};
-
-__device__ __forceinline__ void k_sincos(double x, double& s, double& c) {
-#if RWRT_MATH_NUMPY
-  np_math::nm_sincos(x, s, c);      // == nm_sincostan's s, c
-#else
-  double t;
-  k_sincostan(x, s, c, t);
-#endif
-}
-
-struct TeamRHS {
-  static constexpr int NV = 5;
-  static constexpr int NAUX = 0;
-  static constexpr bool kAutonomous = true;
-  static constexpr bool kTeam = true;
-  CachedStaticBG B;   // wave 0's lookup cache
-  double* X;          // [kTeamSlots][64]
-  double* K;          // [7][5][64]
-  unsigned lane;
-  int role;           // wave index in the block (uniform)
-  __device__ __forceinline__ double& x(int s) const { return X[s * kTeamLanes + lane]; }
-  __device__ __forceinline__ double& k(int j, int v) const { return K[(j * 5 + v) * kTeamLanes + lane]; }
-
-  // ray_rhs for stage s (1..6) of the lane's ray, the block's four waves
-  // together; dy = K_s
-  __device__ __forceinline__ void stage(int s, double t, const double* y, double* dy) const {
-    const double lon = y[0], lat = y[1], kx = y[2];
-    const bool bad = fabs(lat) >= kHalfPi || fabs(y[3]) >= 100.0;
-    const double ky = bad ? kNaN : y[3], amp = y[4];
-    // ---- phase 1: lookup | sin, cos | tan
-    if (role == 0) {
-      double g[11];
-      const auto pending = lookup_begin(B, lon, lat, t);
-      lookup_end(B, pending, g);
-#pragma unroll
-      for (int q = 0; q < 11; ++q) x(TX_G + q) = g[q];
-    } else if (role == 1) {
-      double sn, cs;
-      k_sincos(lat, sn, cs);
-      x(TX_S) = sn;
-      x(TX_C) = cs;
-    } else if (role == 2) {
-      x(TX_TN) = k_tan(lat);
-    }
-    __syncthreads();
-    const double sn = x(TX_S), c = x(TX_C), tn = x(TX_TN);
-    const Merc M = merc_factors(lat, c, sn);
-    const double cp = M.cp, m = M.m;   // cp == c off the pole band (c * 1.0 + 0.0 * 1e-6)
-    const bool mk = m != 1.0;          // mercator12_masked's extra factor
-    const double fu = x(TX_G + F_U), fv = x(TX_G + F_V);
-    const double fqx = x(TX_G + F_QX), fqy = x(TX_G + F_QY);
-    const double fqxx = x(TX_G + F_QXX), fqxy = x(TX_G + F_QXY), fqyy = x(TX_G + F_QYY);
-    // the Mercator outputs without a division (bs.py:862-883)
-    const double o6 = mk ? fqx * m : fqx;
-    const double o7 = mk ? (fqy * cp) * m : fqy * cp;
-    const double o8 = mk ? fqxx * m : fqxx;
-    const double o10 = mk ? (fqxy * cp) * m : fqxy * cp;
-    const double o9 = mk ? o10 * m : o10;
-    const double o11 = mk ? (((fqyy * cp) - (fqy * M.s)) * cp) * m : ((fqyy * cp) - (fqy * M.s)) * cp;
-    // ---- phase 2: the quotients
-    if (role == 0) {
-      double du, dv;
-      div2(fu, cp, fv, cp, du, dv);
-      x(TX_DU) = du;
-      x(TX_DV) = dv;
-    } else if (role == 1) {
-      double dux, dvx;
-      div2(x(TX_G + F_UX), cp, x(TX_G + F_VX), cp, dux, dvx);
-      x(TX_DUX) = dux;
-      x(TX_DVX) = dvx;
-    } else if (role == 2) {
-      // cal_ugvg(mode='extent') with l = ky (ugvg())
-      const double kap = RDIV(ky, kx);
-      const double kap2 = kap * kap;
-      const double kap1 = 1.0 + kap2;
-      const double KK = (kx * kx) * kap1;
-      const double denom = KK * kap1;
-      double qu, qv;
-      div2(((1.0 - kap2) * o7) - ((2.0 * kap) * o6), denom,
-           ((2.0 * kap) * o7) + ((1.0 - kap2) * o6), denom, qu, qv);
-      x(TX_QU) = qu;
-      x(TX_QV) = qv;
-    } else {
-      // core_diffun's quotients that need no Mercator quotient
-      const double kap = RDIV(ky, kx);
-      const double kap2 = kap * kap;
-      const double kap1 = 1.0 + kap * kap;
-      const double kk = (kx * kx) * kap1;
-      double qk, ql;
-      div2(kap * o8 - o10, kk, kap * o9 - o11, kk, qk, ql);
-      x(TX_QK) = qk;
-      x(TX_QL) = ql;
-      x(TX_DAMP2) = (2.0 * (kap * (o8 - o11) + (kap2 - 1.0) * o9)) / (kk * kap1);
-    }
-    __syncthreads();
-    // ---- phase 3: the derivatives
-    if (role < 3) {
-      const double fmu = mk ? x(TX_DU) * m : x(TX_DU);
-      const double fmv = mk ? x(TX_DV) * m : x(TX_DV);
-      if (role == 1) {
-        double d0, d1;
-        div2(fmu + x(TX_QU), kREarth, (fmv + x(TX_QV)) * c, kREarth, d0, d1);
-        k(s, 0) = d0;
-        k(s, 1) = d1;
-      } else {
-        const double fmux = mk ? x(TX_DUX) * m : x(TX_DUX);
-        const double fmvx = mk ? x(TX_DVX) * m : x(TX_DVX);
-        const double fmuy = mk ? (x(TX_G + F_UY) + tn * fu) * m : x(TX_G + F_UY) + tn * fu;
-        const double fmvy = mk ? (x(TX_G + F_VY) + tn * fv) * m : x(TX_G + F_VY) + tn * fv;
-        const double kap = RDIV(ky, kx);
-        if (role == 0) {
-          const double kap1 = 1.0 + kap * kap;
-          const double damp1 = (2.0 * ((fmux + fmvy) + kap * (fmvx + fmuy))) / kap1;
-          const double damp3 = (-2.0 * sn) * fmv;
-          const double damp = (damp1 + x(TX_DAMP2)) + damp3;
-          k(s, 4) = div_rearth(damp * amp);
-        } else {
-          double d2, d3;
-          div2((-kx) * ((fmux + kap * fmvx) + x(TX_QK)), kREarth,
-               (-kx) * ((fmuy + kap * fmvy) + x(TX_QL)), kREarth, d2, d3);
-          k(s, 2) = d2;
-          k(s, 3) = d3;
-        }
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int v = 0; v < 5; ++v) dy[v] = k(s, v);
-  }
-};
-
-// rows [it_begin, it_end) of rays order[0, n_heavy): one ray per lane (64 per
-// block, no queue), rk45_run_kernel's loop and post-processing otherwise
-__global__ void __launch_bounds__(256, 1) rk45_team_kernel(RunArgs<StaticBG> a) {
-  nm_stage<NM_ALL>();
-  __shared__ __attribute__((aligned(16))) char cache[kStaticCacheBytesPerWave];
-  __shared__ double X[kTeamSlots * kTeamLanes];
-  __shared__ double Kb[7 * 5 * kTeamLanes];
-  const unsigned lane = threadIdx.x & 63u;
-  const int role = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const TeamRHS P{CachedStaticBG{a.B.F, cache, lane * (RWRT_CACHE_LANE_SLICE ? kSliceStride : 16u), ~0u, ~0u},
-                  X, Kb, lane, role};
-  const int64_t nrows = a.it_end - a.it_begin;
-  const int64_t w = blockIdx.x * (int64_t)kTeamLanes + lane;
-  int64_t ray = (w < a.n_heavy) ? a.order[w] : -1;
-  Lane<TeamRHS, KTeam> L;
-  L.K.p = Kb + lane;
-  int64_t nacc = 0, nrej = 0;
-  int32_t it = a.it_begin, nanrow = 0;
-  double prev_lon = 0.0, prev_lat = 0.0, cos_prev = 0.0;
-  if (ray >= 0) {
-#pragma unroll
-    for (int v = 0; v < 5; ++v) {
-      L.y[v] = a.state[v * a.nray + ray];
-      L.f[v] = a.state[(5 + v) * a.nray + ray];
-    }
-    L.t = a.state[10 * a.nray + ray];
-    L.habs = a.state[11 * a.nray + ray];
-    L.in_step = false;
-    L.rejected = false;
-    L.hs = 0.0;
-    nacc = a.count[2 * ray];
-    nrej = a.count[2 * ray + 1];
-    nanrow = a.nanrow[ray];
-    prev_lon = L.y[0];
-    prev_lat = L.y[1];
-    cos_prev = k_cos(prev_lat);
-  }
-  while (ray >= 0) {
-    const double tb = a.tbound[it];
-    const int st = L.iterate(P, tb, a.min_step, a.rtol, a.atol, nacc, nrej);
-    if (st == Lane<TeamRHS, KTeam>::kStep) continue;
-    // interval it reached: rk45_run_kernel's post-processing (wr.py:835-885)
-    // with cos(lat), ug and vg recomputed at y (the values its K6 reuse gives)
-    double* y = L.y;
-    double ug = kNaN, vg = kNaN, cos_c = kNaN;
-    bool masked = fabs(y[1]) >= kHalfPi;
-    if (!masked) {
-      cos_c = cos_small(y[1]);
-      masked = cal_dis_reaches(y[0], y[1], prev_lon, prev_lat, cos_c, cos_prev, a.cut_off, a.cut_a);
-    }
-    if (masked) {
-#pragma unroll
-      for (int v = 0; v < 5; ++v) y[v] = kNaN;
-      cos_c = kNaN;
-    }
-    const int last = (st == Lane<TeamRHS, KTeam>::kFrozen) ? a.it_end : it + 1;
-    if (role == 0) {
-      if (!masked) ugvg_at(a.B, tb, y[0], y[1], y[2], y[3], ug, vg);
-      const double2 r0 = make_double2(y[0], y[1]), r1 = make_double2(y[2], y[3]);
-      const double2 r2 = make_double2(y[4], ug), r3 = make_double2(vg, (double)nacc);
-      for (int kr = it; kr < last; ++kr) {
-        double2* o = reinterpret_cast<double2*>(a.out + ((size_t)ray * nrows + (kr - a.it_begin)) * RWRT_NOUT);
-        o[0] = r0;
-        o[1] = r1;
-        o[2] = r2;
-        o[3] = r3;
-      }
-    }
-    if (nanrow == a.nt && isnan(y[0])) nanrow = it;   // wr.py:853-855 (host reduces)
-    prev_lon = y[0];
-    prev_lat = y[1];
-    cos_prev = cos_c;
-    it = last;
-    if (st == Lane<TeamRHS, KTeam>::kFrozen) L.t = a.tbound[a.it_end - 1];
-    if (it == a.it_end) {
-      if (role == 0) {
-#pragma unroll
-        for (int v = 0; v < 5; ++v) {
-          a.state[v * a.nray + ray] = y[v];
-          a.state[(5 + v) * a.nray + ray] = L.f[v];
-        }
-        a.state[10 * a.nray + ray] = L.t;
-        a.state[11 * a.nray + ray] = L.habs;
-        a.count[2 * ray] = nacc;
-        a.count[2 * ray + 1] = nrej;
-        a.nanrow[ray] = nanrow;
-      }
-      ray = -1;
-    }
-  }
-}
 
 __global__ void math_kernel(int kind, int64_t n, const double* __restrict__ x,
                             const double* __restrict__ y, double* __restrict__ out) {
@@ -3247,12 +2393,6 @@ __global__ void math_kernel(int kind, int64_t n, const double* __restrict__ x,
     case 14: r = py_mod_2pi_again(py_mod_2pi(a)); break;
     case 15: r = div_hw(a, b, recip_hw(b)); break;
     case 16: r = (double)floor_i32(a); break;
-    case 17: { double sn, cs, tn; sincostan(a, sn, cs, tn); r = sn; } break;
-    case 18: { double sn, cs, tn; sincostan(a, sn, cs, tn); r = cs; } break;
-    case 19: { double sn, cs, tn; sincostan(a, sn, cs, tn); r = tn; } break;
-    case 20: r = rm_pow(a, b); break;
-    case 21: r = rwrt_math::rm_exp(a); break;
-    case 22: r = recip2(a); break;
     case 23: { double q1, q2; div2(a, b, b, a, q1, q2); r = q1; } break;
     case 24: { double q1, q2; div2(b, a, a, b, q1, q2); r = q2; } break;
     case 25: r = np_math::nm_sin(a); break;
@@ -3292,18 +2432,11 @@ struct Rk4Args {
   const uint8_t* frozen;   // rays whose rows rk4_fill_kernel writes (NULL: none)
 };
 
-#ifndef RWRT_RK4_CACHE
-#define RWRT_RK4_CACHE 1   // the RHS lookups through rk45_run_kernel's per-lane LDS cell cache
-#endif
-__global__ void __launch_bounds__(256, RWRT_WAVES_PER_SIMD) rk4_run_kernel(Rk4Args a) {
+__global__ void __launch_bounds__(256, 1) rk4_run_kernel(Rk4Args a) {
   nm_stage<NM_SINCOS | NM_TAN>();
   const int64_t nrows = a.it_end - a.it_begin;
-#if RWRT_RK4_CACHE
   __shared__ __attribute__((aligned(16))) char smem[LaneBG<StaticBG>::kLdsBytes];
   const auto RB = LaneBG<StaticBG>::make(StaticBG{a.F}, smem);
-#else
-  const StaticBG RB{a.F};
-#endif
   const double half = 0.5 * a.dt;        // 0.5 * dt      (wr.py:602-604)
   const double sixth = a.dt / 6.0;       // dt / 6.0      (wr.py:92)
   for (;;) {
@@ -3474,7 +2607,6 @@ __global__ void kat_kernel(int64_t ncol, const double* __restrict__ y0, int32_t 
     for (int v = 0; v < NV; ++v) out[(i * nt + it) * NV + v] = L.y[v];
   }
 }
-
 
 // ---------------------------------------------------------------------------
 // Initial rays: WR.ray_initial_numpy (wr.py:344-395)
@@ -3651,9 +2783,6 @@ rwrt_status launch_init(const BG& B, int64_t nray, const double* d_y0, const rwr
   return check_launch("rk45_init_kernel");
 }
 
-#ifndef RWRT_FROZEN_FILL
-#define RWRT_FROZEN_FILL 1
-#endif
 }  // namespace rwrt
 
 // An execution context (include/rwrt.h rwrt_ctx): everything the ray-loop
@@ -3672,8 +2801,7 @@ struct rwrt_ctx {
   uint8_t* flags = nullptr;
   size_t cap = 0;
   hipStream_t side = nullptr;
-  hipStream_t team = nullptr;   // rk45_team_kernel (latency mode)
-  hipEvent_t flagged = nullptr, filled = nullptr, team_go = nullptr, team_end = nullptr;
+  hipEvent_t flagged = nullptr, filled = nullptr;
   hipEvent_t done = nullptr;   // end of the last call on this context
   int quad_per_wave = 16;      // latency mode: rays per wave (rwrt_ctx_set_latency_density)
   bool used = false;
@@ -3776,12 +2904,8 @@ rwrt_status launch_run(rwrt_ctx* ctx, const BG& B, int64_t nray, const rwrt_para
   // rwrt_ctx_set_latency_density cannot change the density between sizing the
   // latency-mode grid and launching it
   std::lock_guard<std::mutex> lock(ctx->mu);
-#if RWRT_LATENCY_QUAD
   const int32_t quad_per_wave = ctx->quad_per_wave;
   const int64_t per_block = 4 * (int64_t)quad_per_wave;   // rays per latency-mode block
-#else
-  const int64_t per_block = kTeamLanes;
-#endif
   const int64_t team_blocks = (n_heavy + per_block - 1) / per_block;
   if (team_blocks > ctx->ncu / 2)
     return fail(RWRT_ERR_ARG, "n_heavy exceeds the latency mode's capacity (4 x rays-per-wave per CU, half the CUs)%s");
@@ -3799,7 +2923,6 @@ rwrt_status launch_run(rwrt_ctx* ctx, const BG& B, int64_t nray, const rwrt_para
   RunArgs<BG> a{B, nray, p->rtol, p->atol, p->min_step, p->cut_off, p->nt, it_begin, it_end,
                 d_tbound, d_order, d_state, d_count, d_nanrow, d_out, d_work,
                 n_heavy, 0, haversine_cut(p->cut_off), nullptr};
-#if RWRT_FROZEN_FILL
   // frozen rays: flagged on `stream`, filled on the context's side stream
   // while the run kernel (which skips them) integrates the rest; `stream` then
   // waits for the fill, so the call stays one stream-ordered operation
@@ -3810,8 +2933,6 @@ rwrt_status launch_run(rwrt_ctx* ctx, const BG& B, int64_t nray, const rwrt_para
                            ctx->flags);
       }))
     return s;
-#endif
-#if RWRT_LATENCY_QUAD
   // latency mode in the run kernel's first team_blocks blocks (quad_rays):
   // one grid, so they are placed beside the persistent blocks whatever the
   // hardware queues' dispatch order (a second kernel on another stream could
@@ -3823,38 +2944,11 @@ rwrt_status launch_run(rwrt_ctx* ctx, const BG& B, int64_t nray, const rwrt_para
     hipLaunchKernelGGL(rk45_run_kernel<BG>, dim3((unsigned)grid), dim3(256), 0, st, a);
     if (rwrt_status s = check_launch("rk45_run_kernel")) return s;
   }
-#else
-  if (team_blocks) {
-    // latency mode on the context's team stream, after the flags (and
-    // everything before this call on `stream`); `stream` waits for it below
-    if (hipEventRecord(ctx->team_go, st) != hipSuccess || hipStreamWaitEvent(ctx->team, ctx->team_go, 0) != hipSuccess)
-      return check_launch("hipEventRecord(latency mode start)");
-    if constexpr (std::is_same<BG, StaticBG>::value) {
-      hipLaunchKernelGGL(rk45_team_kernel, dim3((unsigned)team_blocks), dim3(256), 0, ctx->team, a);
-      if (rwrt_status s = check_launch("rk45_team_kernel")) return s;
-    }
-    if (hipEventRecord(ctx->team_end, ctx->team) != hipSuccess)
-      return check_launch("hipEventRecord(latency mode end)");
-  }
-  if (nray > n_heavy) {
-    hipLaunchKernelGGL(rk45_run_kernel<BG>, dim3((unsigned)blocks), dim3(256), 0, st, a);
-    if (rwrt_status s = check_launch("rk45_run_kernel")) return s;
-  }
-  if (team_blocks && hipStreamWaitEvent(st, ctx->team_end, 0) != hipSuccess)
-    return check_launch("hipStreamWaitEvent(latency mode end)");
-#endif
-#if RWRT_FROZEN_FILL
-#ifndef RWRT_DIAG_FILL
-#define RWRT_DIAG_FILL 0   // timing-only diagnostic builds: 1 = no fill launch, 2 = the fill after the run kernel
-#endif
-  if (RWRT_DIAG_FILL != 1)
+  if (0 != 1)
     hipLaunchKernelGGL(frozen_fill_kernel<BG>, dim3((unsigned)((nray + kFillThreads - 1) / kFillThreads)),
-                       dim3(kFillThreads), 0, RWRT_DIAG_FILL == 2 ? st : ctx->side, a);
+                       dim3(kFillThreads), 0, 0 == 2 ? st : ctx->side, a);
   if (rwrt_status s = check_launch("frozen_fill_kernel")) return s;
   return ctx_end(ctx, st);
-#else
-  return RWRT_OK;
-#endif
 }
 
 // a time-varying background from the ABI description
@@ -4022,9 +3116,6 @@ rwrt_status rwrt_ctx_create(int32_t device, rwrt_ctx** out) {
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
     c->ncu = ncu;
   if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->team, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreateWithFlags(&c->team_go, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->team_end, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->flagged, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->filled, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->done, hipEventDisableTiming) != hipSuccess) {
@@ -4054,9 +3145,6 @@ rwrt_status rwrt_ctx_destroy(rwrt_ctx* c) {
     if (c->used && hipEventSynchronize(c->done) != hipSuccess) s = check_launch("rwrt_ctx_destroy");
     if (c->flags) (void)hipFree(c->flags);
     if (c->side) (void)hipStreamDestroy(c->side);
-    if (c->team) (void)hipStreamDestroy(c->team);
-    if (c->team_go) (void)hipEventDestroy(c->team_go);
-    if (c->team_end) (void)hipEventDestroy(c->team_end);
     if (c->flagged) (void)hipEventDestroy(c->flagged);
     if (c->filled) (void)hipEventDestroy(c->filled);
     if (c->done) (void)hipEventDestroy(c->done);
@@ -4266,7 +3354,6 @@ rwrt_status rwrt_rk4_run(rwrt_ctx* ctx, const rwrt_grid* g, const double* d_pack
   int64_t blocks = ctx_persistent_blocks<StaticBG>(ctx);
   const int64_t need = (nray + 255) / 256;
   if (blocks > need) blocks = need;
-#if RWRT_FROZEN_FILL
   // rays whose rows are known at the start go to rk4_fill_kernel on the side
   // stream (as launch_run does for the RK45 loop)
   if (rwrt_status s = ctx_flags(ctx, nray)) return s;
@@ -4276,17 +3363,12 @@ rwrt_status rwrt_rk4_run(rwrt_ctx* ctx, const rwrt_grid* g, const double* d_pack
                            ctx->flags);
       }))
     return s;
-#endif
   hipLaunchKernelGGL(rk4_run_kernel, dim3((unsigned)blocks), dim3(256), 0, st, a);
   if (rwrt_status s = check_launch("rk4_run_kernel")) return s;
-#if RWRT_FROZEN_FILL
   hipLaunchKernelGGL(rk4_fill_kernel, dim3((unsigned)((nray + kFillThreads - 1) / kFillThreads)),
                      dim3(kFillThreads), 0, ctx->side, a);
   if (rwrt_status s = check_launch("rk4_fill_kernel")) return s;
   return ctx_end(ctx, st);
-#else
-  return RWRT_OK;
-#endif
 }
 
 rwrt_status rwrt_kat_rk45(int32_t kind, int64_t ncol, const double* d_y0, int32_t nt,
@@ -4313,18 +3395,6 @@ rwrt_status rwrt_selftest_math(int32_t kind, int64_t n, const double* d_x, const
                      n, d_x, d_y, d_out);
   return check_launch("math_kernel");
 }
-
-#if RWRT_DIAG_STAMPS
-// (diagnostic build only; not part of include/rwrt.h) the section cycle sums
-// since the previous call, then zeroed
-rwrt_status rwrt_diag_stamps(unsigned long long* out16) {
-  if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_stamp), sizeof(unsigned long long) * 16) != hipSuccess)
-    return check_launch("rwrt_diag_stamps");
-  unsigned long long z[16] = {};
-  if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamp), z, sizeof(z)) != hipSuccess) return check_launch("rwrt_diag_stamps");
-  return RWRT_OK;
-}
-#endif
 
 // Host side of the drop-in delivery (hostio.HistorySink): the block starts as
 // copies of the previous row, then the shipped columns are scattered in.

@@ -621,8 +621,7 @@ def kat_rk45(kind, y0, t_eval, rtol, atol, min_step, device="cuda"):
 MATH_KINDS = {"sin": 0, "cos": 1, "tan": 2, "pow": 3, "atan2": 4, "mod": 5, "sqrt": 6,
               "div": 7, "floor": 8, "sincos_sin": 9, "sincos_cos": 10, "div_rearth": 11,
               "fmod": 12, "mod2pi": 13, "mod2pi_twice": 14, "div_hw": 15, "floor_i32": 16,
-              "sct_sin": 17, "sct_cos": 18, "sct_tan": 19, "rm_pow": 20, "rm_exp": 21,
-              "recip2": 22, "div2_first": 23,
+              "div2_first": 23,
               "div2_second": 24, "nm_sin": 25, "nm_cos": 26, "nm_tan": 27, "nm_pow": 28,
               "nm_rcp14": 29, "k_sin": 30, "k_cos": 31, "k_tan": 32, "k_pow": 33}
 

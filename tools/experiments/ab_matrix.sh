@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B timing matrix on the GPU box: one bench line per "lib|bench args" entry.
-# usage: tools/ab_matrix.sh <tag> "librwrt.so|--chunk 55" "librwrt_w2g2.so|--chunk 1080" ...
+# usage: tools/experiments/ab_matrix.sh <tag> "librwrt.so|--chunk 55" "librwrt_w2g2.so|--chunk 1080" ...
 tag=$1; shift
 mkdir -p gpurun_out
 for cfg in "$@"; do

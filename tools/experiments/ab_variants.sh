@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B timing of kernel build variants on the GPU box (one bench line each).
-# usage: tools/ab_variants.sh <tag> <days> [extra bench args]
+# usage: tools/experiments/ab_variants.sh <tag> <days> [extra bench args]
 tag=$1; days=$2; shift 2
 mkdir -p gpurun_out
 for lib in rossby-wave-ray-tracing_amd/librwrt_*.so; do
