@@ -265,7 +265,8 @@ rwrt_status rwrt_kat_rk45(int32_t kind, int64_t ncol, const double* d_y0,
  * division pair (as its first / second quotient), 25/26/27/28 the reference
  * NumPy's sin/cos/tan/power as restated in csrc/np_math.h, 29 the restated
  * VRCP14PD, 30/31/32 sin/cos/tan and 33 pow exactly as the kernels evaluate
- * them.
+ * them, 34 x / y by the RHS's shared-reciprocal division (qdiv) and 35 1.0
+ * where that division is inside its exact range (DivGuard), else 0.0.
  * Lets the tests prove which operations are bit-exact on the GPU (IEEE
  * division, sqrt, fmod) and measure the last-bit agreement of the rest. */
 rwrt_status rwrt_selftest_math(int32_t kind, int64_t n, const double* d_x,

@@ -1016,9 +1016,143 @@ __device__ __forceinline__ void ugvg(double fu, double fv, double fqx, double fq
 }
 
 // ---------------------------------------------------------------------------
+// Shared-reciprocal division.  The RHS divides 16 times by five distinct
+// divisors (cos(lat) four times, k (1 + kap^2)^2 three times, k (1 + kap^2)
+// twice, R five times).  The hardware's IEEE f64 division (the compiler's
+// sequence, div2 above) is: v_div_scale both operands, v_rcp_f64 + two
+// Newton steps on the divisor, q = n r, one FMA remainder correction
+// (v_div_fmas), v_div_fixup.  v_div_scale is the identity unless an operand
+// is near the exponent limits, and then the reciprocal part depends on the
+// divisor alone: formed once (rcp2), shared by its numerators (qdiv: four
+// instructions instead of eleven, and a four-deep chain instead of eleven).
+// qdiv(n, d, rcp2(d)) == n / d bit for bit when the numerator's frexp
+// exponent is in [-899, 600] (|n| in [2^-900, 2^600)) or n is 0, inf or NaN
+// (v_div_fixup's cases, frexp exponent 0), and the divisor's in [-99, 100]
+// (tests/test_gpu_parity.py::test_device_math_exactness, kinds 34-35).
+// DivGuard collects those exponents; a lane outside the range recomputes the
+// RHS tail with IEEE divisions (rhs_tail<false>, a rarely taken branch).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double rcp2(double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  double e = fma(-d, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-d, r, 1.0);
+  return fma(r, e, r);
+}
+__device__ __forceinline__ double qdiv(double n, double d, double r) {
+  const double q = n * r;
+  const double e = fma(-d, q, n);
+  return __builtin_amdgcn_div_fixup(fma(e, r, q), d, n);
+}
+struct DivGuard {
+  int nlo = 0, nhi = 0, dlo = 0, dhi = 0;   // exponent range seen (0: neutral)
+  __device__ __forceinline__ void num(double n) {
+    const int e = __builtin_amdgcn_frexp_exp(n);
+    nlo = ::min(nlo, e);
+    nhi = ::max(nhi, e);
+  }
+  __device__ __forceinline__ void den(double d) {
+    const int e = __builtin_amdgcn_frexp_exp(d);
+    dlo = ::min(dlo, e);
+    dhi = ::max(dhi, e);
+  }
+  __device__ __forceinline__ bool ok() const {
+    return (nlo >= -899) & (nhi <= 600) & (dlo >= -99) & (dhi <= 100);
+  }
+};
+__device__ __forceinline__ double qdiv(double n, double d, double r, DivGuard& G) {
+  G.num(n);
+  return qdiv(n, d, r);
+}
+
+// kap_terms with kap = l / k through the shared-reciprocal division, and the
+// reciprocals of the three divisors it forms (guarded: G)
+struct KapTermsR : KapTerms {
+  double rkk, rk1, rden;   // rcp2 of kk, kap1, denom
+};
+__device__ __forceinline__ KapTermsR kap_terms_r(double k, double l, DivGuard& G) {
+  KapTermsR w;
+  G.den(k);
+  w.kap = qdiv(l, k, rcp2(k), G);
+  w.kap2 = w.kap * w.kap;
+  w.kap1 = 1.0 + w.kap2;
+  w.kk = (k * k) * w.kap1;
+  w.denom = w.kk * w.kap1;
+  G.den(w.kap1);
+  G.den(w.kk);
+  G.den(w.denom);
+  w.rkk = rcp2(w.kk);
+  w.rk1 = rcp2(w.kap1);
+  w.rden = rcp2(w.denom);
+  return w;
+}
+
+// ---------------------------------------------------------------------------
 // The RHS: WR.diffun_numpy (wr.py:492-556) + core_diffun (wr.py:44-82)
 // ---------------------------------------------------------------------------
-//
+// Everything after the lookup and the trigonometry: Mercator (bs.py:856-883),
+// cal_ugvg (wn.py:266-294), core_diffun (wr.py:53-78; freq only feeds the
+// dead ps/up terms) and the / R of wr.py:80-82, with IEEE divisions.
+__device__ __forceinline__ void rhs_tail_ieee(const double g[11], const Merc& M, double s, double c,
+                                              double tn, double kx, double ky, double amp, double* dy,
+                                              double& ug, double& vg) {
+  const KapTerms kw = kap_terms(kx, ky);
+  double o[12];
+  mercator12(g, M, tn, o);
+  const double fmu = o[0], fmv = o[1], fmux = o[2], fmuy = o[3], fmvx = o[4], fmvy = o[5];
+  const double fmqx = o[6], fmqy = o[7], fmqxx = o[8], fmqxy = o[9], fmqyx = o[10], fmqyy = o[11];
+  ugvg(fmu, fmv, fmqx, fmqy, kw, ug, vg);
+  const double kap = kw.kap, kap2 = kw.kap2, kap1 = kw.kap1, kk = kw.kk;
+  double qk, ql;
+  div2(kap * fmqxx - fmqyx, kk, kap * fmqxy - fmqyy, kk, qk, ql);
+  const double dzwn = (-kx) * ((fmux + kap * fmvx) + qk);
+  const double dmwn = (-kx) * ((fmuy + kap * fmvy) + ql);
+  double damp1, damp2;
+  div2(2.0 * ((fmux + fmvy) + kap * (fmvx + fmuy)), kap1,
+       2.0 * (kap * (fmqxx - fmqyy) + (kap2 - 1.0) * fmqxy), kw.denom, damp1, damp2);
+  const double damp3 = (-2.0 * s) * fmv;
+  const double damp = (damp1 + damp2) + damp3;
+  div2(ug, kREarth, vg * c, kREarth, dy[0], dy[1]);     // x / R, x / R
+  div2(dzwn, kREarth, dmwn, kREarth, dy[2], dy[3]);
+  dy[4] = div_rearth(damp * amp);
+}
+// The same operations on the same operands with the shared-reciprocal
+// division; false when a lane must redo them with rhs_tail_ieee (an operand
+// outside qdiv's exact range, or the Mercator pole band).
+__device__ __forceinline__ bool rhs_tail_fast(const double g[11], const Merc& M, double s, double c,
+                                              double tn, double kx, const KapTermsR& kw, DivGuard G,
+                                              double amp, double* dy, double& ug, double& vg) {
+  // Mercator off the pole band (M.m == 1, M.cp == c; mercator12)
+  const double fu = g[F_U], fv = g[F_V];
+  const double rc = rcp2(c);
+  const double fmu = qdiv(fu, c, rc, G), fmv = qdiv(fv, c, rc, G);
+  const double fmux = qdiv(g[F_UX], c, rc, G), fmvx = qdiv(g[F_VX], c, rc, G);
+  const double fmuy = g[F_UY] + tn * fu, fmvy = g[F_VY] + tn * fv;
+  const double fmqx = g[F_QX], fmqy = g[F_QY] * c, fmqxx = g[F_QXX];
+  const double fmqyx = g[F_QXY] * c, fmqxy = fmqyx;
+  const double fmqyy = ((g[F_QYY] * c) - (g[F_QY] * s)) * c;
+  // cal_ugvg
+  const double kap = kw.kap, kap2 = kw.kap2;
+  ug = fmu + qdiv(((1.0 - kap2) * fmqy) - ((2.0 * kap) * fmqx), kw.denom, kw.rden, G);
+  vg = fmv + qdiv(((2.0 * kap) * fmqy) + ((1.0 - kap2) * fmqx), kw.denom, kw.rden, G);
+  // core_diffun
+  const double qk = qdiv(kap * fmqxx - fmqyx, kw.kk, kw.rkk, G);
+  const double ql = qdiv(kap * fmqxy - fmqyy, kw.kk, kw.rkk, G);
+  const double dzwn = (-kx) * ((fmux + kap * fmvx) + qk);
+  const double dmwn = (-kx) * ((fmuy + kap * fmvy) + ql);
+  const double damp1 = qdiv(2.0 * ((fmux + fmvy) + kap * (fmvx + fmuy)), kw.kap1, kw.rk1, G);
+  const double damp2 = qdiv(2.0 * (kap * (fmqxx - fmqyy) + (kap2 - 1.0) * fmqxy), kw.denom, kw.rden, G);
+  const double damp3 = (-2.0 * s) * fmv;
+  const double damp = (damp1 + damp2) + damp3;
+  const double rR = rcp2(kREarth);   // (loop-invariant)
+  dy[0] = qdiv(ug, kREarth, rR, G);
+  dy[1] = qdiv(vg * c, kREarth, rR, G);
+  dy[2] = qdiv(dzwn, kREarth, rR, G);
+  dy[3] = qdiv(dmwn, kREarth, rR, G);
+  dy[4] = qdiv(damp * amp, kREarth, rR, G);
+  return G.ok() & (M.m == 1.0);
+}
+
 // aux (optional) receives {ug, vg, cos(lat)} of this evaluation -- exactly what
 // the per-interval post-processing recomputes at the same position
 // (wr.py:844, 856-865) -- or NaN for a masked ray (no values computed).
@@ -1036,33 +1170,19 @@ __device__ __forceinline__ void ray_rhs(const BG& B, double t, const double* y, 
   // arithmetic (one scheduling region: the refill below is a branch)
   const auto trig = np_math::nm_sincostan_begin(lat);
   double s, c;
-  const KapTerms kw = kap_terms(kx, ky);   // (k, l only: beside the trig and the cell arithmetic)
+  DivGuard G;
+  const KapTermsR kw = kap_terms_r(kx, ky, G);   // (k, l only: beside the trig and the cell arithmetic)
   const auto pending = lookup_begin(B, lon, lat, t);   // the lookup's fill overlaps the trig
   double tn;
   np_math::nm_sincostan_end(lat, trig, s, c, tn);   // == k_sincostan(lat, s, c, tn)
   __builtin_amdgcn_sched_barrier(0);
   lookup_end(B, pending, g);
   const Merc M = merc_factors(lat, c, s);
-  double o[12];
-  mercator12(g, M, tn, o);
-  const double fmu = o[0], fmv = o[1], fmux = o[2], fmuy = o[3], fmvx = o[4], fmvy = o[5];
-  const double fmqx = o[6], fmqy = o[7], fmqxx = o[8], fmqxy = o[9], fmqyx = o[10], fmqyy = o[11];
   double ug, vg;
-  ugvg(fmu, fmv, fmqx, fmqy, kw, ug, vg);
-  // core_diffun (wr.py:53-78); freq only feeds the dead ps/up terms
-  const double kap = kw.kap, kap2 = kw.kap2, kap1 = kw.kap1, kk = kw.kk;
-  double qk, ql;
-  div2(kap * fmqxx - fmqyx, kk, kap * fmqxy - fmqyy, kk, qk, ql);
-  const double dzwn = (-kx) * ((fmux + kap * fmvx) + qk);
-  const double dmwn = (-kx) * ((fmuy + kap * fmvy) + ql);
-  double damp1, damp2;
-  div2(2.0 * ((fmux + fmvy) + kap * (fmvx + fmuy)), kap1,
-       2.0 * (kap * (fmqxx - fmqyy) + (kap2 - 1.0) * fmqxy), kw.denom, damp1, damp2);
-  const double damp3 = (-2.0 * s) * fmv;
-  const double damp = (damp1 + damp2) + damp3;
-  div2(ug, kREarth, vg * c, kREarth, dy[0], dy[1]);     // x / R, x / R
-  div2(dzwn, kREarth, dmwn, kREarth, dy[2], dy[3]);
-  dy[4] = div_rearth(damp * amp);
+  if (!rhs_tail_fast(g, M, s, c, tn, kx, kw, G, amp, dy, ug, vg)) {
+    asm volatile("");   // an operand outside qdiv's exact range, or the pole band (rare branch)
+    rhs_tail_ieee(g, M, s, c, tn, kx, ky, amp, dy, ug, vg);
+  }
   if (aux) {
     aux[0] = ug;
     aux[1] = vg;
@@ -2404,6 +2524,13 @@ __global__ void math_kernel(int kind, int64_t n, const double* __restrict__ x,
     case 31: { double sn, cs, tn; k_sincostan(a, sn, cs, tn); r = cs; } break;
     case 32: { double sn, cs, tn; k_sincostan(a, sn, cs, tn); r = tn; } break;
     case 33: r = k_pow(a, b); break;
+    case 34: r = qdiv(a, b, rcp2(b)); break;   // exact when kind 35 says so
+    case 35: {   // 1 if qdiv(a, b, rcp2(b)) is in DivGuard's exact range, else 0
+      DivGuard G;
+      G.num(a);
+      G.den(b);
+      r = G.ok() ? 1.0 : 0.0;
+    } break;
     default: r = fmod_pos(a, b); break;
   }
   out[i] = r;
@@ -3388,7 +3515,7 @@ rwrt_status rwrt_kat_rk45(int32_t kind, int64_t ncol, const double* d_y0, int32_
 
 rwrt_status rwrt_selftest_math(int32_t kind, int64_t n, const double* d_x, const double* d_y,
                                double* d_out, void* stream) {
-  if (n < 0 || kind < 0 || kind > 33 || (n > 0 && (!d_x || !d_out)))
+  if (n < 0 || kind < 0 || kind > 35 || (n > 0 && (!d_x || !d_out)))
     return fail(RWRT_ERR_ARG, "bad selftest arguments%s");
   if (n == 0) return RWRT_OK;
   hipLaunchKernelGGL(math_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, kind,

@@ -623,7 +623,8 @@ MATH_KINDS = {"sin": 0, "cos": 1, "tan": 2, "pow": 3, "atan2": 4, "mod": 5, "sqr
               "fmod": 12, "mod2pi": 13, "mod2pi_twice": 14, "div_hw": 15, "floor_i32": 16,
               "div2_first": 23,
               "div2_second": 24, "nm_sin": 25, "nm_cos": 26, "nm_tan": 27, "nm_pow": 28,
-              "nm_rcp14": 29, "k_sin": 30, "k_cos": 31, "k_tan": 32, "k_pow": 33}
+              "nm_rcp14": 29, "k_sin": 30, "k_cos": 31, "k_tan": 32, "k_pow": 33,
+              "qdiv": 34, "qdiv_exact_range": 35}
 
 
 def selftest_math(name, x, y=None, device="cuda"):

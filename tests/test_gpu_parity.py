@@ -330,6 +330,31 @@ def test_device_math_exactness():
     assert np.array_equal(selftest_math("div_hw", phys[:n], both), phys[:n] / both)
     assert np.array_equal(np.signbit(selftest_math("div_hw", num, np.full(num.shape, -2.5))),
                           np.signbit(num / -2.5))
+    # the RHS's shared-reciprocal division (qdiv, csrc/rwrt.hip): wherever
+    # DivGuard admits it, bit-identical to IEEE division -- signed zeros,
+    # inf and NaN numerators (v_div_fixup) and NaN / inf / zero divisors
+    # included; physical operands are always admitted
+    specials = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 5e-324, -2.0 ** -1000, 2.0 ** -899,
+                         -2.0 ** -900, 2.0 ** 599, -2.0 ** 600, 1.7e308, 1.0, -3.0])
+    dens = np.array([0.0175, 0.5, 1.0, 6.3712e6, 2.5, -2.5, 2.0 ** -99, 2.0 ** -100, 2.0 ** 99,
+                     2.0 ** 100, 2.0 ** 101, 1e-300, 1e300, 0.0, -0.0, np.inf, -np.inf, np.nan])
+    nn = np.concatenate([wide, phys, np.repeat(specials, 64)])
+    for den in dens:
+        dd = np.full(nn.shape, den)
+        inr = selftest_math("qdiv_exact_range", nn, dd) == 1.0
+        with np.errstate(all="ignore"):
+            want = nn / dd
+        got = selftest_math("qdiv", nn, dd)
+        assert np.array_equal(got[inr], want[inr], equal_nan=True), den
+        m = inr & ~np.isnan(want)
+        assert np.array_equal(np.signbit(got[m]), np.signbit(want[m])), den
+        if 2.0 ** -99 <= abs(den) <= 2.0 ** 99:
+            sp = np.isin(nn, specials[:5]) | np.isnan(nn)
+            assert inr[sp].all(), den              # zeros, inf, NaN: on the fast path
+    ph = rng.standard_normal(n) * 10.0 ** rng.uniform(-40, 40, n)
+    pd = rng.uniform(0.0175, 1.0, n) * 10.0 ** rng.integers(-20, 20, n)
+    assert (selftest_math("qdiv_exact_range", ph, pd) == 1.0).all()
+    assert np.array_equal(selftest_math("qdiv", ph, pd), ph / pd)
     # np.floor(x).astype('int32') (x86 semantics: NaN / out of range -> INT32_MIN)
     fx = np.concatenate([a, [2.0 ** 31 - 1, 2.0 ** 31 - 0.5, 2.0 ** 31, -2.0 ** 31, -2.0 ** 31 - 1,
                              1e300, -1e300, np.inf, -np.inf]])
