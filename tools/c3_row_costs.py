@@ -1,0 +1,59 @@
+"""Per-ray cost profile of the C3 bench schedule (GPU): accepted steps per ray at
+every ``--every``-th row of every launch, to study how well one launch's
+per-ray work predicts the next (the work-queue order of rk45_run_kernel).
+
+Runs the bench's path (shard.run_sharded on one GPU: probe, 24- and
+160-row re-ordering launches, the rest) and writes
+``<out>/c3_rowcost_<bg>.npz``: ``rows`` (row indices sampled), ``nacc``
+``[nslot, len(rows)]`` int32 (running accepted steps, the rows' 8th column),
+``att`` ``[nslot]`` final accepted + rejected attempts, and the launch bounds.
+
+    python tools/c3_row_costs.py [--bg nonzonal zonal] [--every 10]
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "rossby-wave-ray-tracing_amd")]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--bg", nargs="+", default=["nonzonal", "zonal"])
+    ap.add_argument("--every", type=int, default=10)
+    ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out"))
+    a = ap.parse_args()
+    import torch
+    from bench import c3_sources, make_bs
+    from engine import RayEngine
+    from shard import run_sharded
+    os.makedirs(a.out, exist_ok=True)
+    nt = 1081
+    for kind in a.bg:
+        bs, _ = make_bs(kind)
+        eng = RayEngine.from_bs(bs)
+        src, zcs = c3_sources(eng)
+        y0 = torch.cat([eng.initial_rows_dev(src, zc)[0][:5].reshape(5, -1) for zc in zcs], dim=1)
+        cols, rows = [], []
+
+        def sink(i0, i1, o, idx):
+            take = [r for r in range(i0, i1) if r % a.every == 0 or r == i1 - 1]
+            cols.append(o[:, [r - i0 for r in take], 7].to(torch.int32).cpu())
+            rows.extend(take)
+
+        r = run_sharded(eng, y0, nt, 7200.0, rank=0, world=1, probe=6, lead=[24, 160], chunk=nt - 1,
+                        sink=sink, ttotal=(nt - 1) * 7200.0, team="auto")
+        nacc = torch.cat(cols, dim=1).numpy()
+        att = r.counts.sum(1).to(torch.int32).cpu().numpy()
+        np.savez_compressed(os.path.join(a.out, f"c3_rowcost_{kind}.npz"), rows=np.array(rows), nacc=nacc,
+                            att=att, bounds=np.array([[1, 7]] + [list(b) for b in r.res.bounds]))
+        print(kind, nacc.shape, int(att.sum()), flush=True)
+        del eng, r, y0
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
