@@ -289,7 +289,7 @@ def main():
     ap.add_argument("--periods", type=int, default=5, help="C3 periods in the batch (1-5)")
     ap.add_argument("--bg", default="zonal", choices=["zonal", "nonzonal"],
                     help="C3 basic state: the DJF jets (SURVEY.md 8(d)) or their non-zonal variant")
-    ap.add_argument("--order", default="priority", choices=["priority", "cost", "cell", "live"],
+    ap.add_argument("--order", default="priority", choices=["priority", "cost", "cell", "total", "live"],
                     help="work-queue order: longest-first by the previous launch's work (priority, "
                          "cost), cost classes then Morton order of the rays' cells (cell), or live-first")
     ap.add_argument("--probe", type=int, default=6,

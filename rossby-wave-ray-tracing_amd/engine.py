@@ -481,7 +481,7 @@ class RayEngine:
         i0 = start
         # short leading chunks measure the per-ray cost that orders the next one
         lead = [first_chunk] if isinstance(first_chunk, int) else list(first_chunk or [])
-        if order_policy in ("cost", "priority", "cell"):
+        if order_policy in ("cost", "priority", "cell", "total"):
             for n in lead:
                 if 0 < n < chunk and i0 < end:
                     bounds.append((i0, min(i0 + n, end)))
@@ -492,14 +492,15 @@ class RayEngine:
         rows_max = max([b - a for a, b in bounds] or [1])
         bufs = _row_buffers(out, nray, rows_max, self.device)
         order = None
-        if prev_work is None or order_policy not in ("cost", "priority", "cell"):
+        if prev_work is None or order_policy not in ("cost", "priority", "cell", "total"):
             order = self.live_first_order_of(st)
         for k, (i0, i1) in enumerate(bounds):
             flat = bufs[k % len(bufs)].view(-1)
             view = flat[: nray * (i1 - i0) * H.NOUT].view(nray, i1 - i0, H.NOUT)
             work = None
-            if order_policy in ("cost", "priority", "cell") and prev_work is not None:
-                work = cnt.sum(1) - prev_work
+            if order_policy in ("cost", "priority", "cell", "total") and prev_work is not None:
+                # the previous launch's attempts per ray, or ("total") all of them so far
+                work = cnt.sum(1) - (0 if order_policy == "total" else prev_work)
                 order = self.cost_cell_order(st, work) if order_policy == "cell" else self.cost_order(st, work)
             n_heavy, qpw = self.team_size(team, st, work, order, i1 - i0) if team else (0, 16)
             if os.environ.get("RWRT_DEBUG_TEAM"):

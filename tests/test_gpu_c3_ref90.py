@@ -92,3 +92,31 @@ def test_c3_90d_sample_bitwise_with_reference_arithmetic(kind):
 def test_c3_90d_sample_latency_mode_bitwise():
     g, hist, counts = run_c3_90d("zonal", team=1024)
     check(g, hist, counts)
+
+
+@pytest.mark.parametrize("kind", ["zonal", "nonzonal"])
+def test_c3_90d_sample_rk4_bitwise(kind):
+    """The reference's default integrator (fixed-step RK4, wr.py:702-765) on the
+    whole C3 set for 90 days: the same 2 048-ray sample's every row equals the
+    oracle's RK4 history bit for bit."""
+    import torch
+    from bench import c3_sources, make_bs
+    from engine import RayEngine
+    g = golden(f"c3_ref90_{kind}.npz")
+    nt = int(g["nt"])
+    bs, _ = make_bs(kind)
+    eng = RayEngine.from_bs(bs)
+    src, zcs = c3_sources(eng)
+    rows0 = torch.cat([eng.initial_rows_dev(src, zc)[0].reshape(7, -1) for zc in zcs], dim=1)
+    idx = torch.as_tensor(g["idx"], device=eng.device)
+    hist = np.full((7, nt, idx.numel()), np.nan)
+    hist[:, 0] = rows0[:, idx].cpu().numpy()
+
+    def sink(i0, i1, rows):
+        hist[:, i0:i1] = np.transpose(rows[idx][:, :, :7].cpu().numpy(), (2, 1, 0))
+
+    eng.integrate_rk4(rows0[:5].contiguous(), nt, 7200.0, chunk=270, sink=sink)
+    del eng
+    torch.cuda.empty_cache()
+    bad = np.nonzero(row_hashes(hist) != g["rk4_row_sha"])[0]
+    assert not bad.size, f"{bad.size} of {nt} RK4 rows differ, first row {int(bad[0])}"

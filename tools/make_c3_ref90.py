@@ -15,7 +15,9 @@ Each fixture holds the slot indices (bench.c3_initial_state's order), per
 output row the sha256 of the 7 history variables of the sample (``(7, n)``
 fp64, NaN canonicalised; tests/golden/make_devmath.row_hashes), the last row
 in full, per-ray accepted and rejected attempt counts, and the 90-day costs
-used for the pick.
+used for the pick; and the same rows of the reference's default integrator,
+fixed-step RK4 (wr.py:702-765), on the same rays (``rk4_row_sha``,
+``rk4_last``).
 
     python tools/make_c3_ref90.py --costs profiles/r3/c3_cost90 [--bg zonal nonzonal]
 """
@@ -38,10 +40,12 @@ TSTEP = 7200.0
 def _run(args):
     bg, y0, row0 = args
     import rwrt_oracle as O
+    ob = O.Background(**bg)
     with np.errstate(all="ignore"):
-        hist, nacc, nrej, st = O.ray_run(O.Background(**bg), y0, NT, TSTEP, row0=row0)
-    assert st == 0
-    return hist, nacc, nrej
+        hist, nacc, nrej, st = O.ray_run(ob, y0, NT, TSTEP, row0=row0)
+        hist4, st4 = O.ray_run_rk4(ob, y0.copy(), NT, TSTEP, row0=row0)
+    assert st == 0 and st4 == 0
+    return hist, nacc, nrej, hist4
 
 
 def pick(cost, heavy, strata, per, seed=0):
@@ -81,16 +85,18 @@ def main():
         with mp.get_context("spawn").Pool(a.procs) as pool:
             res = pool.map(_run, jobs)
         hist = np.empty((7, NT, idx.size))
+        hist4 = np.empty((7, NT, idx.size))
         nacc = np.empty(idx.size, np.int64)
         nrej = np.empty(idx.size, np.int64)
-        for k, (h, na, nr) in enumerate(res):
+        for k, (h, na, nr, h4) in enumerate(res):
             sel = np.arange(k, idx.size, a.procs)
-            hist[:, :, sel], nacc[sel], nrej[sel] = h, na, nr
+            hist[:, :, sel], nacc[sel], nrej[sel], hist4[:, :, sel] = h, na, nr, h4
         assert np.array_equal(nacc + nrej, cost[idx]), "GPU cost survey disagrees with the oracle"
         out = os.path.join(ROOT, "tests", "golden", f"c3_ref90_{kind}.npz")
         np.savez_compressed(out, idx=idx.astype(np.int64), nt=np.int64(NT), nslot=np.int64(cost.size),
                             row_sha=row_hashes(hist), last=hist[:, -1], nacc=nacc, nrej=nrej,
-                            cost90=cost[idx].astype(np.int32), heavy=np.int64(a.heavy))
+                            cost90=cost[idx].astype(np.int32), heavy=np.int64(a.heavy),
+                            rk4_row_sha=row_hashes(hist4), rk4_last=hist4[:, -1])
         print(f"{kind}: {idx.size} rays ({a.heavy} heaviest: {int(cost[idx].max())} attempts max), "
               f"{int(nacc.sum())} accepted steps, alive at 90 d: {int((~np.isnan(hist[0, -1])).sum())}, "
               f"{time.time() - t0:.0f} s -> {os.path.relpath(out, ROOT)}", flush=True)
