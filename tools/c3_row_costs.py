@@ -24,7 +24,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--bg", nargs="+", default=["nonzonal", "zonal"])
     ap.add_argument("--every", type=int, default=10)
-    ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out"))
+    ap.add_argument("--out", default="/tmp/rwrt_rowcost")
     a = ap.parse_args()
     import torch
     from bench import c3_sources, make_bs
