@@ -97,56 +97,6 @@ __device__ __forceinline__ void div2(double a1, double b1, double a2, double b2,
       : "vcc");
 }
 
-// ---------------------------------------------------------------------------
-// Shared-reciprocal division.  The RHS divides 16 times by five distinct
-// divisors (cos(lat) four times, k (1 + kap^2)^2 three times, k (1 + kap^2)
-// twice, R five times).  The hardware's IEEE f64 division (the compiler's
-// sequence, div2 above) is: v_div_scale both operands, v_rcp_f64 + two
-// Newton steps on the divisor, q = n r, one FMA remainder correction
-// (v_div_fmas), v_div_fixup.  v_div_scale is the identity unless an operand
-// is near the exponent limits, and then the reciprocal part depends on the
-// divisor alone: formed once (rcp2), shared by its numerators (qdiv: four
-// instructions instead of eleven, and a four-deep chain instead of eleven).
-// qdiv(n, d, rcp2(d)) == n / d bit for bit when the numerator's frexp
-// exponent is in [-899, 600] (|n| in [2^-900, 2^600)) or n is 0, inf or NaN
-// (v_div_fixup's cases, frexp exponent 0), and the divisor's in [-99, 100]
-// (tests/test_gpu_parity.py::test_device_math_exactness, kinds 34-35).
-// DivGuard collects those exponents; a lane outside the range redoes its
-// divisions with IEEE division (rhs_tail_ieee, cell_coords: rare branches).
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ double rcp2(double d) {
-  double r = __builtin_amdgcn_rcp(d);
-  double e = fma(-d, r, 1.0);
-  r = fma(r, e, r);
-  e = fma(-d, r, 1.0);
-  return fma(r, e, r);
-}
-__device__ __forceinline__ double qdiv(double n, double d, double r) {
-  const double q = n * r;
-  const double e = fma(-d, q, n);
-  return __builtin_amdgcn_div_fixup(fma(e, r, q), d, n);
-}
-struct DivGuard {
-  int nlo = 0, nhi = 0, dlo = 0, dhi = 0;   // exponent range seen (0: neutral)
-  __device__ __forceinline__ void num(double n) {
-    const int e = __builtin_amdgcn_frexp_exp(n);
-    nlo = ::min(nlo, e);
-    nhi = ::max(nhi, e);
-  }
-  __device__ __forceinline__ void den(double d) {
-    const int e = __builtin_amdgcn_frexp_exp(d);
-    dlo = ::min(dlo, e);
-    dhi = ::max(dhi, e);
-  }
-  __device__ __forceinline__ bool ok() const {
-    return (nlo >= -899) & (nhi <= 600) & (dlo >= -99) & (dhi <= 100);
-  }
-};
-__device__ __forceinline__ double qdiv(double n, double d, double r, DivGuard& G) {
-  G.num(n);
-  return qdiv(n, d, r);
-}
-
 // rkf45.py:604-615 (Dormand-Prince 5(4)); C++ constant division is IEEE
 // correctly rounded, like Python's.
 constexpr double kC[6] = {0.0, 1.0 / 5, 3.0 / 10, 4.0 / 5, 8.0 / 9, 1.0};
@@ -291,30 +241,11 @@ struct Corners {
   unsigned oa, ob, oc, od; // element offsets of a, b, c, d from F.P
 };
 
-// The fractional cell coordinates (lon - lon0) / dlon, (lat - lat0) / dlat
-// (interpolation.py:80-82): the shared-reciprocal division with the grid
-// spacings' reciprocals (wave-uniform, hoisted out of the ray loop); the
-// interleaved IEEE pair for numerators outside qdiv's exact range (rare).
-__device__ __forceinline__ void cell_coords(double nx, double dlon, double ny, double dlat, double& x,
-                                            double& y) {
-  x = qdiv(nx, dlon, rcp2(dlon));
-  y = qdiv(ny, dlat, rcp2(dlat));
-  DivGuard G;
-  G.num(nx);
-  G.num(ny);
-  G.den(dlon);
-  G.den(dlat);
-  if (!G.ok()) {
-    asm volatile("");   // (rare branch)
-    div2(nx, dlon, ny, dlat, x, y);
-  }
-}
-
 __device__ __forceinline__ Corners corners(const Field& F, double lon, double lat) {
   // lon arrives already reduced once (bs.py:519); interpolation.py:80 reduces again.
   const double lons = py_mod_2pi_again(lon);
   double x, y;
-  cell_coords(lons - F.lon0, F.dlon, lat - F.lat0, F.dlat, x, y);
+  div2(lons - F.lon0, F.dlon, lat - F.lat0, F.dlat, x, y);
   const int ix = floor_i32(x), iy = floor_i32(y);
   const int x0 = clip(ix, F.W - 1), x1 = clip(inc_i32(ix), F.W - 1);
   const int y0 = clip(iy, F.H - 1), y1 = clip(inc_i32(iy), F.H - 1);
@@ -553,7 +484,7 @@ struct VaryingBG {
                                        unsigned& key_x, unsigned& key_y) const {
     const double lons = py_mod_2pi_again(py_mod_2pi(lon));
     double x, y;
-    cell_coords(lons - lon0, dlon, lat - lat0, dlat, x, y);
+    div2(lons - lon0, dlon, lat - lat0, dlat, x, y);
     const int ix = floor_i32(x), iy = floor_i32(y);
     const int x0 = clip(ix, W - 1), x1 = clip(inc_i32(ix), W - 1);
     const int y0 = clip(iy, H - 1), y1 = clip(inc_i32(iy), H - 1);
@@ -1082,6 +1013,56 @@ __device__ __forceinline__ void ugvg(double fu, double fv, double fqx, double fq
 __device__ __forceinline__ void ugvg(double fu, double fv, double fqx, double fqy,
                                      double k, double l, double& ug, double& vg) {
   ugvg(fu, fv, fqx, fqy, kap_terms(k, l), ug, vg);
+}
+
+// ---------------------------------------------------------------------------
+// Shared-reciprocal division.  The RHS divides 16 times by five distinct
+// divisors (cos(lat) four times, k (1 + kap^2)^2 three times, k (1 + kap^2)
+// twice, R five times).  The hardware's IEEE f64 division (the compiler's
+// sequence, div2 above) is: v_div_scale both operands, v_rcp_f64 + two
+// Newton steps on the divisor, q = n r, one FMA remainder correction
+// (v_div_fmas), v_div_fixup.  v_div_scale is the identity unless an operand
+// is near the exponent limits, and then the reciprocal part depends on the
+// divisor alone: formed once (rcp2), shared by its numerators (qdiv: four
+// instructions instead of eleven, and a four-deep chain instead of eleven).
+// qdiv(n, d, rcp2(d)) == n / d bit for bit when the numerator's frexp
+// exponent is in [-899, 600] (|n| in [2^-900, 2^600)) or n is 0, inf or NaN
+// (v_div_fixup's cases, frexp exponent 0), and the divisor's in [-99, 100]
+// (tests/test_gpu_parity.py::test_device_math_exactness, kinds 34-35).
+// DivGuard collects those exponents; a lane outside the range recomputes the
+// RHS tail with IEEE divisions (rhs_tail<false>, a rarely taken branch).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double rcp2(double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  double e = fma(-d, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-d, r, 1.0);
+  return fma(r, e, r);
+}
+__device__ __forceinline__ double qdiv(double n, double d, double r) {
+  const double q = n * r;
+  const double e = fma(-d, q, n);
+  return __builtin_amdgcn_div_fixup(fma(e, r, q), d, n);
+}
+struct DivGuard {
+  int nlo = 0, nhi = 0, dlo = 0, dhi = 0;   // exponent range seen (0: neutral)
+  __device__ __forceinline__ void num(double n) {
+    const int e = __builtin_amdgcn_frexp_exp(n);
+    nlo = ::min(nlo, e);
+    nhi = ::max(nhi, e);
+  }
+  __device__ __forceinline__ void den(double d) {
+    const int e = __builtin_amdgcn_frexp_exp(d);
+    dlo = ::min(dlo, e);
+    dhi = ::max(dhi, e);
+  }
+  __device__ __forceinline__ bool ok() const {
+    return (nlo >= -899) & (nhi <= 600) & (dlo >= -99) & (dhi <= 100);
+  }
+};
+__device__ __forceinline__ double qdiv(double n, double d, double r, DivGuard& G) {
+  G.num(n);
+  return qdiv(n, d, r);
 }
 
 // kap_terms with kap = l / k through the shared-reciprocal division, and the
