@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--bg", nargs="+", default=["nonzonal", "zonal"])
     ap.add_argument("--every", type=int, default=10)
     ap.add_argument("--out", default="/tmp/rwrt_rowcost")
+    ap.add_argument("--features", default=None, help="directory for the compact per-live-ray feature file")
     a = ap.parse_args()
     import torch
     from bench import c3_sources, make_bs
@@ -37,12 +38,13 @@ def main():
         eng = RayEngine.from_bs(bs)
         src, zcs = c3_sources(eng)
         y0 = torch.cat([eng.initial_rows_dev(src, zc)[0][:5].reshape(5, -1) for zc in zcs], dim=1)
-        cols, rows = [], []
+        cols, rows, ends = [], [], {}
 
         def sink(i0, i1, o, idx):
             take = [r for r in range(i0, i1) if r % a.every == 0 or r == i1 - 1]
             cols.append(o[:, [r - i0 for r in take], 7].to(torch.int32).cpu())
             rows.extend(take)
+            ends[i1 - 1] = o[:, -1, :7].to(torch.float32).cpu()   # the launch's last row
 
         r = run_sharded(eng, y0, nt, 7200.0, rank=0, world=1, probe=6, lead=[24, 160], chunk=nt - 1,
                         sink=sink, ttotal=(nt - 1) * 7200.0, team="auto")
@@ -50,6 +52,15 @@ def main():
         att = r.counts.sum(1).to(torch.int32).cpu().numpy()
         np.savez_compressed(os.path.join(a.out, f"c3_rowcost_{kind}.npz"), rows=np.array(rows), nacc=nacc,
                             att=att, bounds=np.array([[1, 7]] + [list(b) for b in r.res.bounds]))
+        if a.features:
+            # a compact per-live-ray feature set for studying cost predictors
+            live = np.nonzero(att > 0)[0]
+            live = np.sort(np.random.default_rng(0).choice(live, size=min(len(live), 250000), replace=False))
+            feat = {f"row{r}": ends[r].numpy()[live][:, :4] for r in sorted(ends) if r < nt - 1}
+            np.savez_compressed(os.path.join(a.features, f"c3_features_{kind}.npz"), slot=live.astype(np.int32),
+                                att=att[live], rows=np.array(rows),
+                                nacc=nacc[live][:, [k for k, r in enumerate(rows) if r % 90 == 0 or r in ends]],
+                                nacc_rows=np.array([r for r in rows if r % 90 == 0 or r in ends]), **feat)
         print(kind, nacc.shape, int(att.sum()), flush=True)
         del eng, r, y0
         torch.cuda.empty_cache()
