@@ -306,6 +306,9 @@ def main():
                          "levels and an fp32 RHS (fp64 positions, time and stepper)")
     ap.add_argument("--c5-periods", type=int, default=5,
                     help="C5 periods (1-5 of the C3 list; 5 = 9.67 M slots, ~4 M live rays: BASELINE's size)")
+    ap.add_argument("--split", default="auto", choices=["auto", "off"],
+                    help="split the long launch once more when the leading launches' per-ray work "
+                         "predicts the next poorly (RayEngine.SPLIT_RHO)")
     ap.add_argument("--team", default="auto",
                     help="rays per launch in latency mode (quad_rays: four lanes of a wave per ray); "
                          "an integer or 'auto' (RayEngine.team_size)")
@@ -409,6 +412,7 @@ def main():
     out = torch.empty((n_local, min(chunk, nt - 1), 8), dtype=torch.float64, device=dev)
     lead = [int(x) for x in str(args.first_chunk).split(",") if x]
     team = args.team if args.team == "auto" else int(args.team)
+    split = None if args.split == "off" else args.split
     gather_dev = torch.device("cpu") if backend == "gloo" else dev
     n_live_max = n_live
     if weak and dist:
@@ -439,12 +443,12 @@ def main():
         if weak:
             r = run_sharded(eng, y, nt, 7200.0, rank=0, world=1, probe=args.probe, lead=lead,
                             chunk=chunk, out=out, events=events, ttotal=(nt - 1) * 7200.0,
-                            order_policy=args.order, team=team)
+                            order_policy=args.order, team=team, split=split)
             gather_endpoints(r)
             return r
         return run_sharded(eng, y, nt, 7200.0, group=group, probe=args.probe, lead=lead,
                            chunk=chunk, out=out, events=events, ttotal=(nt - 1) * 7200.0,
-                           order_policy=args.order, team=team)
+                           order_policy=args.order, team=team, split=split)
 
     for _ in range(args.warmup):
         one_step()
@@ -520,6 +524,8 @@ def main():
             "init_bitwise_vs_host": init_same,
             "endpoints_rank0_sha256": endpoint_sha(ends0) if ends0 is not None else None,
             "queue_order": args.order,
+            "long_launch_split": {"mode": args.split, "rank_corr_of_leading_launches": eng.split_rho,
+                                  "threshold": eng.SPLIT_RHO, "rows": eng.SPLIT_ROWS},
             "library": os.path.basename(os.environ.get("RWRT_LIB", "librwrt.so")),
             "library_sha256": library_sha(),
             "roofline": roofline(per_launch_steps, avg_launch_s, workload, schedule, BYTES_PER_STEP, args),

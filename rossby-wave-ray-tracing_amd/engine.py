@@ -70,6 +70,7 @@ class RayEngine:
         self.work = torch.zeros(4, dtype=torch.int32, device=self.device)
 
     bg = None   # rwrt_background of a time-varying state (None: the reference's static state)
+    split_rho = None   # the last advance()'s rank correlation of its leading launches (split="auto")
     _ctx = None
 
     @property
@@ -460,14 +461,44 @@ class RayEngine:
                             group=group, order_policy=order_policy, first_chunk=first_chunk,
                             n_live=n_live, n_live_local=n_live_local, team=team, stop_row=stop_row)
 
+    # Adaptive split of the long launch after the leading ones (split="auto"):
+    # a launch is list scheduling of its rays on the lanes in the queue order,
+    # so its makespan is as good as the previous launch's per-ray work
+    # predicts this one's.  When the two leading launches' per-ray work
+    # correlates weakly (rank correlation below SPLIT_RHO: the non-zonal C3,
+    # ~0.5, against ~0.8 on the zonal jets), the rest is split once after
+    # SPLIT_ROWS rows and re-ordered by the work so far there
+    # (tools/c3_predictors.py, profiles/r3/sched/: the non-zonal last launch
+    # runs 1.66x its throughput bound in the predicted order, 1.00x in the
+    # actual one; one split: +5 %).
+    SPLIT_RHO = 0.7
+    SPLIT_ROWS = 300
+
+    @staticmethod
+    def rank_corr(a, b, mask):
+        """Spearman rank correlation of ``a`` and ``b`` over ``mask`` (device)."""
+        a, b = a[mask].to(F64), b[mask].to(F64)
+        n = a.numel()
+        if n < 3:
+            return 1.0
+        ar = torch.arange(n, dtype=F64, device=a.device)
+        ra, rb = torch.empty_like(a), torch.empty_like(b)
+        ra[torch.argsort(a, stable=True)] = ar
+        rb[torch.argsort(b, stable=True)] = ar
+        ra, rb = ra - ra.mean(), rb - rb.mean()
+        den = torch.sqrt((ra * ra).sum() * (rb * rb).sum())
+        return float(((ra * rb).sum() / den).item()) if den > 0 else 1.0
+
     def advance(self, st, p, tb, start, chunk=None, sink=None, out=None, events=None, group=None,
                 order_policy="priority", first_chunk=None, n_live=None, n_live_local=None,
-                prev_work=None, team=0, stop_row=None):
+                prev_work=None, team=0, stop_row=None, split=None):
         """Rows ``[start, nt)`` of the ray loop for an initialised state ``st``
         (``init``, or a shard of one: ``take``), in time chunks; the body of
         ``integrate``.  ``prev_work`` (each ray's attempt count, accepted +
         rejected, at the start of an earlier launch) orders the first launch
-        longest-first by the attempts since; otherwise live rays go first."""
+        longest-first by the attempts since; otherwise live rays go first.
+        ``split`` ("auto", see SPLIT_RHO) may split the launch after the
+        leading ones once more."""
         nt = int(p.nt)
         end = nt if stop_row is None else max(int(start), min(int(stop_row), nt))
         nray = st["nray"]
@@ -486,6 +517,7 @@ class RayEngine:
                 if 0 < n < chunk and i0 < end:
                     bounds.append((i0, min(i0 + n, end)))
                     i0 = bounds[-1][1]
+        n_lead = len(bounds)
         while i0 < end:
             bounds.append((i0, min(i0 + chunk, end)))
             i0 = bounds[-1][1]
@@ -494,7 +526,23 @@ class RayEngine:
         order = None
         if prev_work is None or order_policy not in ("cost", "priority", "cell", "total"):
             order = self.live_first_order_of(st)
-        for k, (i0, i1) in enumerate(bounds):
+        works = []          # per-ray attempts of the launches so far (the last two)
+        self.split_rho = None
+        k = 0
+        while k < len(bounds):
+            i0, i1 = bounds[k]
+            if (split == "auto" and k == n_lead and len(works) == 2 and i1 - i0 > 2 * self.SPLIT_ROWS
+                    and order_policy in ("cost", "priority", "total")):
+                live = ~torch.isnan(st["state"][:5].sum(0))
+                rho = self.rank_corr(works[0], works[1], live)
+                self.split_rho = rho
+                if rho < self.SPLIT_RHO:
+                    bounds[k:k + 1] = [(i0, i0 + self.SPLIT_ROWS), (i0 + self.SPLIT_ROWS, i1)]
+                    i1 = i0 + self.SPLIT_ROWS
+                    order_policy = "total"
+                if os.environ.get("RWRT_DEBUG_SCHED"):
+                    print(f"split: rank correlation {rho:.3f} -> {'split' if rho < self.SPLIT_RHO else 'one launch'}",
+                          flush=True)
             flat = bufs[k % len(bufs)].view(-1)
             view = flat[: nray * (i1 - i0) * H.NOUT].view(nray, i1 - i0, H.NOUT)
             work = None
@@ -513,8 +561,11 @@ class RayEngine:
                 events.append((e0, e1))
             else:
                 self.run(st, p, tb, i0, i1, view, order, n_heavy, qpw)
+            if split == "auto" and k < n_lead:
+                works = (works + [cnt.sum(1) - prev_work])[-2:]
             if sink is not None:
                 sink(i0, i1, view)
+            k += 1
         mx = int(st["nanrow"].max().item()) if nray else 0
         if group is not None:
             from shard import reduce_max

@@ -207,7 +207,7 @@ class ShardedRun:
 
 def run_sharded(eng, y0, nt, tstep=7200.0, group=None, rank=None, world=None, probe=6,
                 lead=(24, 96), chunk=None, out=None, sink=None, events=None, gather=True,
-                ttotal=None, order_policy="priority", team=0):
+                ttotal=None, order_policy="priority", team=0, split=None):
     """One ray set ``y0[5, nray]`` (identical on every rank) integrated across
     the ranks of ``group``.
 
@@ -217,7 +217,8 @@ def run_sharded(eng, y0, nt, tstep=7200.0, group=None, rank=None, world=None, pr
     Each rank then integrates only its own rays to ``nt`` and ``gather`` sends
     their last row and step counters to rank 0 (RCCL ``gather`` on device
     tensors).  ``sink(i0, i1, rows, idx)`` receives this rank's rows.
-    ``team`` is ``RayEngine.advance``'s latency-mode size per launch.
+    ``team`` is ``RayEngine.advance``'s latency-mode size per launch, ``split``
+    its adaptive split of the long launch.
     ``rank``/``world`` without a group emulate one rank of a larger job on
     this device (single-GPU rehearsal: no collectives).  Rays are independent
     and both global couplings are decided over every ray, so the union of the
@@ -258,7 +259,7 @@ def run_sharded(eng, y0, nt, tstep=7200.0, group=None, rank=None, world=None, pr
     res = eng.advance(local, p, tb, 1 + npr, chunk=chunk, sink=keep, out=out, events=events,
                       group=group, order_policy=order_policy, first_chunk=list(lead),
                       n_live=int(summary[0]), n_live_local=n_live_local,
-                      prev_work=torch.zeros_like(cost[idx]), team=team)
+                      prev_work=torch.zeros_like(cost[idx]), team=team, split=split)
     steps_local = int(local["count"][:, 0].sum().item())
     ends = cnts = None
     if gather:
