@@ -289,9 +289,11 @@ def main():
     ap.add_argument("--periods", type=int, default=5, help="C3 periods in the batch (1-5)")
     ap.add_argument("--bg", default="zonal", choices=["zonal", "nonzonal"],
                     help="C3 basic state: the DJF jets (SURVEY.md 8(d)) or their non-zonal variant")
-    ap.add_argument("--order", default="priority", choices=["priority", "cost", "cell", "total", "live"],
+    ap.add_argument("--order", default=None, choices=["priority", "cost", "cell", "total", "live"],
                     help="work-queue order: longest-first by the previous launch's work (priority, "
-                         "cost), cost classes then Morton order of the rays' cells (cell), or live-first")
+                         "cost; C3's default), cost classes then Morton order of the rays' cells (cell; "
+                         "C5's default: its lookups are HBM gathers), by all work so far (total), or "
+                         "live-first")
     ap.add_argument("--probe", type=int, default=6,
                     help="rows of the probe launch over every ray whose attempts split and order the set")
     ap.add_argument("--first-chunk", default=None,
@@ -318,6 +320,8 @@ def main():
     ap.add_argument("--replicate", type=int, default=1,
                     help="diagnostic: repeat the ray batch k times (more rays per lane)")
     args = ap.parse_args()
+    if args.order is None:
+        args.order = "cell" if args.config == "C5" else "priority"
     how, world = resolve_world(args.gpus)
     if how == "spawn":
         # no launcher: start the N ranks here, before anything touches the GPU
@@ -739,6 +743,7 @@ def main_c5(args, dist, group, rank, world, dev, share=1):
             "ray_steps_per_step": tot_steps / args.steps,
             "rejected_per_accepted": tot_rej * args.steps / max(tot_steps, 1),
             "levels_build_s": t_build,
+            "queue_order": args.order,
             "library_sha256": library_sha(),
             "init": "GPU rwrt_ray_initial inside every timed step",
             "roofline": roofline(per_launch_steps, avg_launch_s, workload, schedule, bps, args)}))
