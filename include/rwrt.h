@@ -99,6 +99,14 @@ rwrt_status rwrt_ctx_destroy(rwrt_ctx* ctx);
  * other rays' cell refills and interval ends) at more CUs per heavy ray.
  * Schedule only: results do not depend on it. */
 rwrt_status rwrt_ctx_set_latency_density(rwrt_ctx* ctx, int32_t rays_per_wave);
+/* Diagnostic ray trace of the context's rwrt_rk45_run calls (NULL / 0: off):
+ * for queue positions w < capacity of the order, the ray's lane records
+ * d_trace[w * 8 + 0..7] = {ray, hardware id (HW_REG_HW_ID: wave, SIMD, CU, SE
+ * fields), XCC id, start and end of the ray's integration in the launch
+ * (s_memrealtime, 100 MHz), attempts made, 1 if in latency mode else 0,
+ * block index} -- where and how long the heaviest rays run (the makespan of
+ * a launch is theirs).  Costs one compare per ray when off. */
+rwrt_status rwrt_ctx_set_trace(rwrt_ctx* ctx, int64_t* d_trace, int64_t capacity);
 /* Last error message of the calling thread ("" if none). */
 const char* rwrt_last_error(void);
 

@@ -1833,7 +1833,25 @@ struct RunArgs {
   double cut_a;         // haversine argument certainly below cut_off (cal_dis_below)
   const uint8_t* frozen;  // rays frozen at the launch start (NULL: none skipped), see frozen_fill_kernel
   int32_t quad_per_wave = 16;  // latency mode: rays per wave (1..16; fewer = less divergence per ray)
+  int64_t* trace = nullptr;    // diagnostic ray trace (rwrt_ctx_set_trace), positions < trace_cap
+  int64_t trace_cap = 0;
 };
+
+// rwrt_ctx_set_trace: where (HW_ID, XCC) and when a traced ray ran
+__device__ __forceinline__ void trace_ray(int64_t* tr, int64_t w, int64_t ray, uint64_t t0, int64_t attempts,
+                                          bool latency) {
+  const unsigned hw = __builtin_amdgcn_s_getreg(4 | (31 << 11));    // HW_REG_HW_ID, 32 bits
+  const unsigned xcc = __builtin_amdgcn_s_getreg(20 | (15 << 11));  // HW_REG_XCC_ID
+  int64_t* r = tr + w * 8;
+  r[0] = ray;
+  r[1] = hw;
+  r[2] = xcc;
+  r[3] = (int64_t)t0;
+  r[4] = (int64_t)__builtin_amdgcn_s_memrealtime();
+  r[5] = attempts;
+  r[6] = latency ? 1 : 0;
+  r[7] = blockIdx.x;
+}
 
 // Haversine threshold: d = 2 atan2(sqrt(a), sqrt(1 - a)) increases with a, so
 // a < sin^2(cut_off / 2) (1 - 1e-9) proves d < cut_off for the computed d too
@@ -2139,6 +2157,8 @@ __device__ __forceinline__ void quad_rays(const RunArgs<StaticBG>& a, char* cach
   }
   double t = a.state[10 * a.nray + ray], habs = a.state[11 * a.nray + ray], hs = 0.0;
   int64_t nacc = a.count[2 * ray], nrej = a.count[2 * ray + 1];
+  const int64_t att0 = nacc + nrej;
+  const uint64_t t_start = a.trace ? __builtin_amdgcn_s_memrealtime() : 0;
   int32_t nanrow = a.nanrow[ray];
   int32_t it = a.it_begin;
   double prev_lon = y[0], prev_lat = y[1], cos_prev = k_cos(prev_lat);
@@ -2242,6 +2262,7 @@ __device__ __forceinline__ void quad_rays(const RunArgs<StaticBG>& a, char* cach
     a.count[2 * ray] = nacc;
     a.count[2 * ray + 1] = nrej;
     a.nanrow[ray] = nanrow;
+    if (a.trace && w < a.trace_cap) trace_ray(a.trace, w, ray, t_start, nacc + nrej - att0, true);
   }
 }
 
@@ -2275,7 +2296,7 @@ __global__ void __launch_bounds__(256, 1) rk45_run_kernel(RunArgs<BG> a) {
   L.K.p = reinterpret_cast<double*>(smem) + threadIdx.x;
   L.K.stride = 256;
   int64_t ray = -1, nacc = 0, nrej = 0;
-  int32_t it = 0, nanrow = 0;
+  int32_t it = 0, nanrow = 0, wpos = 0;   // (wpos: the ray's queue position, for the diagnostic trace)
   double prev_lon = 0.0, prev_lat = 0.0, cos_prev = 0.0;
   if (1) {
     // above frozen_fill_kernel's waves (priority 0) sharing the SIMD: the
@@ -2286,7 +2307,10 @@ __global__ void __launch_bounds__(256, 1) rk45_run_kernel(RunArgs<BG> a) {
     if (ray < 0) {
       const int64_t w = a.n_heavy + atomicAdd(&a.queue[1], 1);
       if (w >= a.nray) break;
+      wpos = (int32_t)w;
       ray = a.order ? a.order[w] : w;
+      if (a.trace && w < a.trace_cap)   // (diagnostic) the ray's start
+        a.trace[w * 8 + 3] = (int64_t)__builtin_amdgcn_s_memrealtime();
       if (a.frozen && a.frozen[ray]) {   // its rows come from frozen_fill_kernel
         ray = -1;
         continue;
@@ -2378,6 +2402,9 @@ __global__ void __launch_bounds__(256, 1) rk45_run_kernel(RunArgs<BG> a) {
       }
       a.state[10 * a.nray + ray] = L.t;
       a.state[11 * a.nray + ray] = L.habs;
+      if (a.trace && wpos < a.trace_cap)   // (diagnostic)
+        trace_ray(a.trace, wpos, ray, a.trace[wpos * 8 + 3], nacc + nrej - a.count[2 * ray] - a.count[2 * ray + 1],
+                  false);
       a.count[2 * ray] = nacc;
       a.count[2 * ray + 1] = nrej;
       a.nanrow[ray] = nanrow;
@@ -2931,6 +2958,8 @@ struct rwrt_ctx {
   hipEvent_t flagged = nullptr, filled = nullptr;
   hipEvent_t done = nullptr;   // end of the last call on this context
   int quad_per_wave = 16;      // latency mode: rays per wave (rwrt_ctx_set_latency_density)
+  int64_t* trace = nullptr;    // rwrt_ctx_set_trace (diagnostic)
+  int64_t trace_cap = 0;
   bool used = false;
   std::mutex mu;
 };
@@ -3066,6 +3095,10 @@ rwrt_status launch_run(rwrt_ctx* ctx, const BG& B, int64_t nray, const rwrt_para
   // wait for a CU on its XCD until the persistent grid drains)
   a.heavy_blocks = (int32_t)team_blocks;
   a.quad_per_wave = quad_per_wave;
+  if constexpr (std::is_same<BG, StaticBG>::value) {
+    a.trace = ctx->trace;
+    a.trace_cap = ctx->trace ? ctx->trace_cap : 0;
+  }
   if (nray > n_heavy || team_blocks) {
     const int64_t grid = team_blocks + (nray > n_heavy ? blocks : 0);
     hipLaunchKernelGGL(rk45_run_kernel<BG>, dim3((unsigned)grid), dim3(256), 0, st, a);
@@ -3259,6 +3292,16 @@ rwrt_status rwrt_ctx_set_latency_density(rwrt_ctx* c, int32_t rays_per_wave) {
   if (rays_per_wave < 1 || rays_per_wave > 16) return fail(RWRT_ERR_ARG, "rays_per_wave must be 1..16%s");
   std::lock_guard<std::mutex> lock(c->mu);
   c->quad_per_wave = rays_per_wave;
+  return RWRT_OK;
+}
+
+rwrt_status rwrt_ctx_set_trace(rwrt_ctx* c, int64_t* d_trace, int64_t capacity) {
+  if (!c) return fail(RWRT_ERR_ARG, "rwrt_ctx is NULL%s");
+  if (capacity < 0 || (capacity > 0 && !d_trace) || capacity > 0x7fffffffLL)
+    return fail(RWRT_ERR_ARG, "trace capacity out of range or NULL trace buffer%s");
+  std::lock_guard<std::mutex> lock(c->mu);
+  c->trace = capacity ? d_trace : nullptr;
+  c->trace_cap = capacity;
   return RWRT_OK;
 }
 
