@@ -101,11 +101,12 @@ rwrt_status rwrt_ctx_destroy(rwrt_ctx* ctx);
 rwrt_status rwrt_ctx_set_latency_density(rwrt_ctx* ctx, int32_t rays_per_wave);
 /* Diagnostic ray trace of the context's rwrt_rk45_run calls (NULL / 0: off):
  * for queue positions w < capacity of the order, the ray's lane records
- * d_trace[w * 8 + 0..7] = {ray, hardware id (HW_REG_HW_ID: wave, SIMD, CU, SE
- * fields), XCC id, start and end of the ray's integration in the launch
+ * d_trace[w * 10 + 0..9] = {ray, hardware id (HW_REG_HW_ID: wave, SIMD, CU,
+ * SE fields), XCC id, start and end of the ray's integration in the launch
  * (s_memrealtime, 100 MHz), attempts made, 1 if in latency mode else 0,
- * block index} -- where and how long the heaviest rays run (the makespan of
- * a launch is theirs).  Costs one compare per ray when off. */
+ * block index, start and end in shader clocks (s_memtime)} -- where, how long
+ * and at what clock the heaviest rays run (the makespan of a launch is
+ * theirs).  Costs one compare per ray when off. */
 rwrt_status rwrt_ctx_set_trace(rwrt_ctx* ctx, int64_t* d_trace, int64_t capacity);
 /* Last error message of the calling thread ("" if none). */
 const char* rwrt_last_error(void);

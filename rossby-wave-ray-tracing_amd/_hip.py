@@ -156,7 +156,7 @@ class Context:
 
     def set_trace(self, trace=None):
         """Diagnostic ray trace (rwrt_ctx_set_trace): ``trace`` an int64 device
-        tensor ``[cap, 8]`` (None: off)."""
+        tensor ``[cap, 10]`` (None: off)."""
         if trace is None:
             check(load().rwrt_ctx_set_trace(self._h, None, 0))
         else:

@@ -1838,19 +1838,23 @@ struct RunArgs {
 };
 
 // rwrt_ctx_set_trace: where (HW_ID, XCC) and when a traced ray ran
-__device__ __forceinline__ void trace_ray(int64_t* tr, int64_t w, int64_t ray, uint64_t t0, int64_t attempts,
-                                          bool latency) {
+constexpr int kTraceWords = 10;
+__device__ __forceinline__ void trace_start(int64_t* tr, int64_t w) {
+  tr[w * kTraceWords + 3] = (int64_t)__builtin_amdgcn_s_memrealtime();
+  tr[w * kTraceWords + 8] = (int64_t)__builtin_amdgcn_s_memtime();
+}
+__device__ __forceinline__ void trace_ray(int64_t* tr, int64_t w, int64_t ray, int64_t attempts, bool latency) {
   const unsigned hw = __builtin_amdgcn_s_getreg(4 | (31 << 11));    // HW_REG_HW_ID, 32 bits
   const unsigned xcc = __builtin_amdgcn_s_getreg(20 | (15 << 11));  // HW_REG_XCC_ID
-  int64_t* r = tr + w * 8;
+  int64_t* r = tr + w * kTraceWords;
   r[0] = ray;
   r[1] = hw;
   r[2] = xcc;
-  r[3] = (int64_t)t0;
-  r[4] = (int64_t)__builtin_amdgcn_s_memrealtime();
+  r[4] = (int64_t)__builtin_amdgcn_s_memrealtime();   // (r[3], r[8]: trace_start)
   r[5] = attempts;
   r[6] = latency ? 1 : 0;
   r[7] = blockIdx.x;
+  r[9] = (int64_t)__builtin_amdgcn_s_memtime();       // shader clock: r[9]-r[8] cycles over r[4]-r[3]
 }
 
 // Haversine threshold: d = 2 atan2(sqrt(a), sqrt(1 - a)) increases with a, so
@@ -2158,7 +2162,7 @@ __device__ __forceinline__ void quad_rays(const RunArgs<StaticBG>& a, char* cach
   double t = a.state[10 * a.nray + ray], habs = a.state[11 * a.nray + ray], hs = 0.0;
   int64_t nacc = a.count[2 * ray], nrej = a.count[2 * ray + 1];
   const int64_t att0 = nacc + nrej;
-  const uint64_t t_start = a.trace ? __builtin_amdgcn_s_memrealtime() : 0;
+  if (a.trace && w < a.trace_cap && R.role == 0) trace_start(a.trace, w);
   int32_t nanrow = a.nanrow[ray];
   int32_t it = a.it_begin;
   double prev_lon = y[0], prev_lat = y[1], cos_prev = k_cos(prev_lat);
@@ -2262,7 +2266,7 @@ __device__ __forceinline__ void quad_rays(const RunArgs<StaticBG>& a, char* cach
     a.count[2 * ray] = nacc;
     a.count[2 * ray + 1] = nrej;
     a.nanrow[ray] = nanrow;
-    if (a.trace && w < a.trace_cap) trace_ray(a.trace, w, ray, t_start, nacc + nrej - att0, true);
+    if (a.trace && w < a.trace_cap) trace_ray(a.trace, w, ray, nacc + nrej - att0, true);
   }
 }
 
@@ -2309,8 +2313,7 @@ __global__ void __launch_bounds__(256, 1) rk45_run_kernel(RunArgs<BG> a) {
       if (w >= a.nray) break;
       wpos = (int32_t)w;
       ray = a.order ? a.order[w] : w;
-      if (a.trace && w < a.trace_cap)   // (diagnostic) the ray's start
-        a.trace[w * 8 + 3] = (int64_t)__builtin_amdgcn_s_memrealtime();
+      if (a.trace && w < a.trace_cap) trace_start(a.trace, w);   // (diagnostic)
       if (a.frozen && a.frozen[ray]) {   // its rows come from frozen_fill_kernel
         ray = -1;
         continue;
@@ -2403,8 +2406,7 @@ __global__ void __launch_bounds__(256, 1) rk45_run_kernel(RunArgs<BG> a) {
       a.state[10 * a.nray + ray] = L.t;
       a.state[11 * a.nray + ray] = L.habs;
       if (a.trace && wpos < a.trace_cap)   // (diagnostic)
-        trace_ray(a.trace, wpos, ray, a.trace[wpos * 8 + 3], nacc + nrej - a.count[2 * ray] - a.count[2 * ray + 1],
-                  false);
+        trace_ray(a.trace, wpos, ray, nacc + nrej - a.count[2 * ray] - a.count[2 * ray + 1], false);
       a.count[2 * ray] = nacc;
       a.count[2 * ray + 1] = nrej;
       a.nanrow[ray] = nanrow;

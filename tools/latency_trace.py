@@ -30,13 +30,15 @@ def decode(tr, n):
     """Trace rows -> list of dicts (HW_ID fields per the gfx9 layout)."""
     out = []
     for w in range(n):
-        ray, hw, xcc, t0, t1, att, lat, blk = (int(x) for x in tr[w])
+        ray, hw, xcc, t0, t1, att, lat, blk, c0, c1 = (int(x) for x in tr[w])
         if att <= 0 or t1 <= 0:
             continue
         out.append({"pos": w, "ray": ray, "xcc": xcc & 0xF, "se": (hw >> 13) & 7, "cu": (hw >> 8) & 0xF,
                     "sh": (hw >> 12) & 1, "simd": (hw >> 4) & 3, "wave": hw & 0xF, "block": blk,
                     "latency_mode": bool(lat), "attempts": att, "t0": t0, "t1": t1,
-                    "s": (t1 - t0) / 1e8, "us_per_attempt": 1e6 * (t1 - t0) / 1e8 / att})
+                    "s": (t1 - t0) / 1e8, "us_per_attempt": 1e6 * (t1 - t0) / 1e8 / att,
+                    "clock_GHz": (c1 - c0) / ((t1 - t0) / 1e8) / 1e9 if t1 > t0 else None,
+                    "kcycles_per_attempt": (c1 - c0) / att / 1e3})
     return out
 
 
@@ -49,6 +51,11 @@ def summary(rays):
     return {"traced": len(rays), "slowest": s[:5],
             "max_s": s[0]["s"], "median_us_per_attempt": float(np.median([r["us_per_attempt"] for r in rays])),
             "xccs": dict(Counter(r["xcc"] for r in rays)), "max_rays_per_cu": max(cu.values()),
+            "clock_GHz_by_xcc": {x: float(np.median([r["clock_GHz"] for r in rays if r["xcc"] == x]))
+                                 for x in sorted({r["xcc"] for r in rays})},
+            "us_per_attempt_by_xcc": {x: float(np.median([r["us_per_attempt"] for r in rays if r["xcc"] == x]))
+                                      for x in sorted({r["xcc"] for r in rays})},
+            "kcycles_per_attempt_median": float(np.median([r["kcycles_per_attempt"] for r in rays])),
             "max_rays_per_simd": max(simd.values()), "cus": len(cu)}
 
 
@@ -67,7 +74,7 @@ def main():
     src, zcs = c3_sources(eng)
     y0 = torch.cat([eng.initial_rows_dev(src, zc)[0][:5].reshape(5, -1) for zc in zcs], dim=1)
     cap = 256
-    trace = torch.zeros((cap, 8), dtype=torch.int64, device=eng.device)
+    trace = torch.zeros((cap, 10), dtype=torch.int64, device=eng.device)
     res = {}
     work = None
     for case in a.cases.split(","):
