@@ -2134,6 +2134,7 @@ __device__ __forceinline__ bool quad_dis_reaches(const QuadRole& R, double lon_c
 // dispatch order of concurrent kernels), in the run kernel's LDS: the cell
 // cache where the run kernel keeps it, the owned stage values (20 KB) where
 // the run kernel keeps its stages.
+template <bool kTrace>
 __device__ __forceinline__ void quad_rays(const RunArgs<StaticBG>& a, char* cache, double* Kq) {
   const CachedStaticBG B = LaneBG<StaticBG>::make(a.B, cache);
   QuadRole R;
@@ -2162,7 +2163,7 @@ __device__ __forceinline__ void quad_rays(const RunArgs<StaticBG>& a, char* cach
   double t = a.state[10 * a.nray + ray], habs = a.state[11 * a.nray + ray], hs = 0.0;
   int64_t nacc = a.count[2 * ray], nrej = a.count[2 * ray + 1];
   const int64_t att0 = nacc + nrej;
-  if (a.trace && w < a.trace_cap && R.role == 0) trace_start(a.trace, w);
+  if (kTrace && w < a.trace_cap && R.role == 0) trace_start(a.trace, w);
   int32_t nanrow = a.nanrow[ray];
   int32_t it = a.it_begin;
   double prev_lon = y[0], prev_lat = y[1], cos_prev = k_cos(prev_lat);
@@ -2266,7 +2267,7 @@ __device__ __forceinline__ void quad_rays(const RunArgs<StaticBG>& a, char* cach
     a.count[2 * ray] = nacc;
     a.count[2 * ray + 1] = nrej;
     a.nanrow[ray] = nanrow;
-    if (a.trace && w < a.trace_cap) trace_ray(a.trace, w, ray, nacc + nrej - att0, true);
+    if (kTrace && w < a.trace_cap) trace_ray(a.trace, w, ray, nacc + nrej - att0, true);
   }
 }
 
@@ -2279,7 +2280,9 @@ __device__ __forceinline__ void quad_rays(const RunArgs<StaticBG>& a, char* cach
 // latency mode (quad_rays in the grid's first blocks, order[0, n_heavy)); the
 // queue is the rest.
 using KStore = KShared<5>;
-template <class BG>
+// kTrace: the diagnostic instantiation (rwrt_ctx_set_trace) -- the product
+// kernel carries none of the trace hooks
+template <class BG, bool kTrace = false>
 __global__ void __launch_bounds__(256, 1) rk45_run_kernel(RunArgs<BG> a) {
   nm_stage<NM_ALL>();
   using LBG = typename LaneBG<BG>::type;
@@ -2290,7 +2293,7 @@ __global__ void __launch_bounds__(256, 1) rk45_run_kernel(RunArgs<BG> a) {
   if constexpr (std::is_same<BG, StaticBG>::value) {
     if ((int)blockIdx.x < a.heavy_blocks) {   // (block-uniform) latency mode
       if (1) __builtin_amdgcn_s_setprio(1);
-      quad_rays(a, smem + kKBytes, reinterpret_cast<double*>(smem));
+      quad_rays<kTrace>(a, smem + kKBytes, reinterpret_cast<double*>(smem));
       return;
     }
   }
@@ -2300,7 +2303,7 @@ __global__ void __launch_bounds__(256, 1) rk45_run_kernel(RunArgs<BG> a) {
   L.K.p = reinterpret_cast<double*>(smem) + threadIdx.x;
   L.K.stride = 256;
   int64_t ray = -1, nacc = 0, nrej = 0;
-  int32_t it = 0, nanrow = 0, wpos = 0;   // (wpos: the ray's queue position, for the diagnostic trace)
+  int32_t it = 0, nanrow = 0, wpos = 0;   // (wpos: the ray's queue position, kTrace only)
   double prev_lon = 0.0, prev_lat = 0.0, cos_prev = 0.0;
   if (1) {
     // above frozen_fill_kernel's waves (priority 0) sharing the SIMD: the
@@ -2311,9 +2314,11 @@ __global__ void __launch_bounds__(256, 1) rk45_run_kernel(RunArgs<BG> a) {
     if (ray < 0) {
       const int64_t w = a.n_heavy + atomicAdd(&a.queue[1], 1);
       if (w >= a.nray) break;
-      wpos = (int32_t)w;
       ray = a.order ? a.order[w] : w;
-      if (a.trace && w < a.trace_cap) trace_start(a.trace, w);   // (diagnostic)
+      if (kTrace) {
+        wpos = (int32_t)w;
+        if (w < a.trace_cap) trace_start(a.trace, w);
+      }
       if (a.frozen && a.frozen[ray]) {   // its rows come from frozen_fill_kernel
         ray = -1;
         continue;
@@ -2405,7 +2410,7 @@ __global__ void __launch_bounds__(256, 1) rk45_run_kernel(RunArgs<BG> a) {
       }
       a.state[10 * a.nray + ray] = L.t;
       a.state[11 * a.nray + ray] = L.habs;
-      if (a.trace && wpos < a.trace_cap)   // (diagnostic)
+      if (kTrace && wpos < a.trace_cap)
         trace_ray(a.trace, wpos, ray, nacc + nrej - a.count[2 * ray] - a.count[2 * ray + 1], false);
       a.count[2 * ray] = nacc;
       a.count[2 * ray + 1] = nrej;
@@ -3103,7 +3108,12 @@ rwrt_status launch_run(rwrt_ctx* ctx, const BG& B, int64_t nray, const rwrt_para
   }
   if (nray > n_heavy || team_blocks) {
     const int64_t grid = team_blocks + (nray > n_heavy ? blocks : 0);
-    hipLaunchKernelGGL(rk45_run_kernel<BG>, dim3((unsigned)grid), dim3(256), 0, st, a);
+    if (a.trace) {
+      if constexpr (std::is_same<BG, StaticBG>::value)
+        hipLaunchKernelGGL((rk45_run_kernel<BG, true>), dim3((unsigned)grid), dim3(256), 0, st, a);
+    } else {
+      hipLaunchKernelGGL(rk45_run_kernel<BG>, dim3((unsigned)grid), dim3(256), 0, st, a);
+    }
     if (rwrt_status s = check_launch("rk45_run_kernel")) return s;
   }
   if (0 != 1)
