@@ -311,6 +311,8 @@ def main():
     ap.add_argument("--split", default="auto", choices=["auto", "off"],
                     help="split the long launch once more when the leading launches' per-ray work "
                          "predicts the next poorly (RayEngine.SPLIT_RHO)")
+    ap.add_argument("--slice", type=int, default=0,
+                    help="rows per work item of the ray loop's queue (rwrt_ctx_set_slicing; 0: one item per ray)")
     ap.add_argument("--team", default="auto",
                     help="rays per launch in latency mode (quad_rays: four lanes of a wave per ray); "
                          "an integer or 'auto' (RayEngine.team_size)")
@@ -383,6 +385,7 @@ def main():
     if args.replicate > 1:
         y0 = np.concatenate([y0] * args.replicate, axis=1)
     eng = RayEngine.from_bs(bs, device=dev)
+    eng.ctx.set_slicing(args.slice)
     nt = int(round(args.days * 12)) + 1
     gpu_init = args.replicate == 1
     init_same = None
@@ -513,6 +516,7 @@ def main():
             "config": {"workload": workload,
                        "ray_slots": nslot * (world if weak else 1), "live_rays_rank0": n_live,
                        "rows": nt, "rows_per_launch": chunk, "launch_rows": schedule,
+                       "slice_rows": args.slice,
                        "rank0_rays": n_mine,
                        "latency_mode": ("per launch, the heaviest rays whose move to quad_rays (four lanes of a "
                                         "wave per ray) minimises the predicted makespan by >= 10 %"
@@ -647,6 +651,7 @@ def main_c5(args, dist, group, rank, world, dev, share=1):
     torch.cuda.synchronize()
     t_build = time.perf_counter() - t_build
     eng = RayEngine.from_levels(lv)
+    eng.ctx.set_slicing(args.slice)
     cfg = S.config("C5")
     deg2rad = np.pi / 180.0
     ix, iy = np.meshgrid(np.arange(cfg.nnx), np.arange(cfg.nny))
@@ -736,7 +741,7 @@ def main_c5(args, dist, group, rank, world, dev, share=1):
             "config": {"workload": workload, "ray_slots": nslot, "live_rays": n_live,
                        "rows": nt, "levels": nlev, "field_storage": args.fields,
                        "level_bytes": int(lv.packed[0].numel() * lv.packed.element_size()),
-                       "rows_per_launch": chunk, "launch_rows": schedule,
+                       "rows_per_launch": chunk, "launch_rows": schedule, "slice_rows": args.slice,
                        "parallelism": (f"{world} rank(s), each its own C5 seed grid (shifted by rank/N deg)"
                                        if weak else f"one ray set over {world} GPU(s) (run_sharded, as C3/C4)")},
             "parity_sample_vs_oracle": parity,

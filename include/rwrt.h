@@ -99,6 +99,17 @@ rwrt_status rwrt_ctx_destroy(rwrt_ctx* ctx);
  * other rays' cell refills and interval ends) at more CUs per heavy ray.
  * Schedule only: results do not depend on it. */
 rwrt_status rwrt_ctx_set_latency_density(rwrt_ctx* ctx, int32_t rays_per_wave);
+/* Row slicing of the context's rwrt_rk45_run / rwrt_rk45_run_tv calls
+ * (0 = off, the default).  A call's rows are cut into slices of slice_rows
+ * rows and every (ray, slice) is one work item: the queue hands out slice 0 of
+ * every queued ray in the d_order order, then slice 1, and so on; a ray's
+ * next slice starts, on whichever lane takes it, once its previous slice has
+ * ended (the solver state moves through the context's scratch, 132 B per
+ * queued ray).  A ray whose work grows late in the call then no longer
+ * starts its remaining work late: the call's tail is one slice of its
+ * heaviest rays instead of their whole remaining work, without the drains of
+ * separate calls.  Schedule only: results do not depend on it. */
+rwrt_status rwrt_ctx_set_slicing(rwrt_ctx* ctx, int32_t slice_rows);
 /* Diagnostic ray trace of the context's rwrt_rk45_run calls (NULL / 0: off):
  * for queue positions w < capacity of the order, the ray's lane records
  * d_trace[w * 10 + 0..9] = {ray, hardware id (HW_REG_HW_ID: wave, SIMD, CU,

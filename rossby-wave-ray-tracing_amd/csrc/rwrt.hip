@@ -1835,7 +1835,35 @@ struct RunArgs {
   int32_t quad_per_wave = 16;  // latency mode: rays per wave (1..16; fewer = less divergence per ray)
   int64_t* trace = nullptr;    // diagnostic ray trace (rwrt_ctx_set_trace), positions < trace_cap
   int64_t trace_cap = 0;
+  // row slicing (rwrt_ctx_set_slicing): work items (queue position, slice)
+  int32_t slice_rows = 0;      // 0: one item per ray, rows [it_begin, it_end)
+  int32_t nslices = 1;
+  const int64_t* qlen = nullptr;   // [1] queued positions that hold a ray live at the start (queue_extent_kernel)
+  int32_t* progress = nullptr;     // [qlen] slices ended per position (kSliceFrozen: frozen, rows written)
+  uint64_t* handoff = nullptr;     // [qlen][16] the ray's solver state between its slices
 };
+
+// Sliced work queue (rwrt_ctx_set_slicing).  A ray's state moves between the
+// lanes that run its slices through one 128-B record per queue position:
+// words 0-4 y, 5-9 f, 10 t, 11 h_abs, 12 accepted, 13 rejected, 14 nanrow.
+// Every access to the records and to the progress words inside the launch is
+// agent-coherent (sc1: __hip_atomic_* relaxed, agent scope); the lane that
+// ends a slice waits for its record stores (vmcnt(0)) before it publishes the
+// slice's end (MI355X_MICROARCH.md, inter-workgroup visibility: sc1 payload,
+// drained, then an sc1 flag; the consumer polls sc1 and loads sc1).
+constexpr int32_t kSliceFrozen = 0x7fffffff;
+__device__ __forceinline__ void hand_put(uint64_t* rec, int j, uint64_t v) {
+  __hip_atomic_store(rec + j, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t hand_get(const uint64_t* rec, int j) {
+  return __hip_atomic_load(const_cast<uint64_t*>(rec) + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void hand_putd(uint64_t* rec, int j, double v) { hand_put(rec, j, (uint64_t)__double_as_longlong(v)); }
+__device__ __forceinline__ double hand_getd(const uint64_t* rec, int j) { return __longlong_as_double((long long)hand_get(rec, j)); }
+__device__ __forceinline__ void slice_publish(int32_t* progress, int64_t q, int32_t v) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the record's stores have completed
+  __hip_atomic_store(progress + q, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // rwrt_ctx_set_trace: where (HW_ID, XCC) and when a traced ray ran
 constexpr int kTraceWords = 10;
@@ -2305,6 +2333,13 @@ __global__ void __launch_bounds__(256, 1) rk45_run_kernel(RunArgs<BG> a) {
   int64_t ray = -1, nacc = 0, nrej = 0;
   int32_t it = 0, nanrow = 0, wpos = 0;   // (wpos: the ray's queue position, kTrace only)
   double prev_lon = 0.0, prev_lat = 0.0, cos_prev = 0.0;
+  // work items: one per queued ray, or (rwrt_ctx_set_slicing) one per (queue
+  // position, slice): slice 0 of every position in the order, then slice 1, ...
+  const bool sliced = a.slice_rows > 0;
+  const int64_t nq = sliced ? *a.qlen : a.nray - a.n_heavy;
+  const int64_t n_items = sliced ? nq * a.nslices : nq;
+  int64_t pend = -1, qpos = 0;   // pend: an item claimed while its ray's previous slice still runs
+  int32_t it_stop = a.it_end;
   if (1) {
     // above frozen_fill_kernel's waves (priority 0) sharing the SIMD: the
     // fill takes the issue cycles the ray loop leaves idle
@@ -2312,31 +2347,65 @@ __global__ void __launch_bounds__(256, 1) rk45_run_kernel(RunArgs<BG> a) {
   }
   for (;;) {
     if (ray < 0) {
-      const int64_t w = a.n_heavy + atomicAdd(&a.queue[1], 1);
-      if (w >= a.nray) break;
-      ray = a.order ? a.order[w] : w;
+      int64_t c = pend;
+      if (c < 0) {
+        c = atomicAdd(&a.queue[1], 1);
+        if (c >= n_items) break;
+      }
+      pend = -1;
+      int32_t k = 0;
+      int64_t q = c;
+      if (sliced) {
+        k = (int32_t)(c / nq);
+        q = c - (int64_t)k * nq;
+      }
+      const int64_t w = a.n_heavy + q;
+      const int64_t r = a.order ? a.order[w] : w;
       if (kTrace) {
         wpos = (int32_t)w;
-        if (w < a.trace_cap) trace_start(a.trace, w);
+        if (k == 0 && w < a.trace_cap) trace_start(a.trace, w);
       }
-      if (a.frozen && a.frozen[ray]) {   // its rows come from frozen_fill_kernel
-        ray = -1;
-        continue;
+      if (a.frozen && a.frozen[r]) continue;   // its rows come from frozen_fill_kernel
+      if (k > 0) {
+        const int32_t done = __hip_atomic_load(a.progress + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (done == kSliceFrozen) continue;    // frozen in an earlier slice: its rows are written
+        if (done < k) {                        // the previous slice still runs: look again next iteration
+          pend = c;
+          continue;
+        }
       }
+      ray = r;
+      qpos = q;
+      it = a.it_begin + k * a.slice_rows;
+      it_stop = sliced ? min(it + a.slice_rows, a.it_end) : a.it_end;
+      if (k == 0) {
 #pragma unroll
-      for (int v = 0; v < 5; ++v) {
-        L.y[v] = a.state[v * a.nray + ray];
-        L.f[v] = a.state[(5 + v) * a.nray + ray];
+        for (int v = 0; v < 5; ++v) {
+          L.y[v] = a.state[v * a.nray + ray];
+          L.f[v] = a.state[(5 + v) * a.nray + ray];
+        }
+        L.t = a.state[10 * a.nray + ray];
+        L.habs = a.state[11 * a.nray + ray];
+        nacc = a.count[2 * ray];
+        nrej = a.count[2 * ray + 1];
+        nanrow = a.nanrow[ray];
+      } else {
+        asm volatile("");   // (a ray's later slice: its state from the hand-off record)
+        const uint64_t* rec = a.handoff + q * 16;
+#pragma unroll
+        for (int v = 0; v < 5; ++v) {
+          L.y[v] = hand_getd(rec, v);
+          L.f[v] = hand_getd(rec, 5 + v);
+        }
+        L.t = hand_getd(rec, 10);
+        L.habs = hand_getd(rec, 11);
+        nacc = (int64_t)hand_get(rec, 12);
+        nrej = (int64_t)hand_get(rec, 13);
+        nanrow = (int32_t)hand_get(rec, 14);
       }
-      L.t = a.state[10 * a.nray + ray];
-      L.habs = a.state[11 * a.nray + ray];
       L.in_step = false;
       L.rejected = false;
       L.hs = 0.0;
-      nacc = a.count[2 * ray];
-      nrej = a.count[2 * ray + 1];
-      nanrow = a.nanrow[ray];
-      it = a.it_begin;
       prev_lon = L.y[0];   // == rlon[it-1], rlat[it-1] (wr.py:844, 877-885)
       prev_lat = L.y[1];
       cos_prev = k_cos(prev_lat);
@@ -2415,6 +2484,23 @@ __global__ void __launch_bounds__(256, 1) rk45_run_kernel(RunArgs<BG> a) {
       a.count[2 * ray] = nacc;
       a.count[2 * ray + 1] = nrej;
       a.nanrow[ray] = nanrow;
+      // frozen before the last slice: its later slices are skipped
+      if (sliced && it_stop < a.it_end) slice_publish(a.progress, qpos, kSliceFrozen);
+      ray = -1;
+    } else if (it == it_stop) {
+      asm volatile("");   // (sliced: the end of one of the ray's slices, not the call's)
+      uint64_t* rec = a.handoff + qpos * 16;
+#pragma unroll
+      for (int v = 0; v < 5; ++v) {
+        hand_putd(rec, v, y[v]);
+        hand_putd(rec, 5 + v, L.f[v]);
+      }
+      hand_putd(rec, 10, L.t);
+      hand_putd(rec, 11, L.habs);
+      hand_put(rec, 12, (uint64_t)nacc);
+      hand_put(rec, 13, (uint64_t)nrej);
+      hand_put(rec, 14, (uint64_t)(int64_t)nanrow);
+      slice_publish(a.progress, qpos, (it - a.it_begin) / a.slice_rows);
       ray = -1;
     }
   }
@@ -2441,6 +2527,27 @@ __global__ void frozen_flag_kernel(const double* __restrict__ state, int64_t nra
     for (int v = 1; v < 5; ++v) sum = sum + state[v * nray + i];
     frozen[i] = isnan(sum / 5.0) ? 1 : 0;   // Lane::iterate's NaN-mean test
   }
+}
+
+// Sliced queue (rwrt_ctx_set_slicing): the queue positions that hold a ray
+// live at the call's start end at qlen[0] -- one past the last such position
+// of the order after the latency-mode entries (any order; the engine's put
+// the frozen rays last), so that a round of slices does not walk the frozen
+// rays (70 % of C3's slots).  qlen[0] is zeroed before.
+__global__ void queue_extent_kernel(const int64_t* __restrict__ order, int64_t nray, int64_t n_heavy,
+                                    const uint8_t* __restrict__ frozen, unsigned long long* __restrict__ qlen) {
+  unsigned long long m = 0;
+  for (int64_t p = n_heavy + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < nray;
+       p += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = order ? order[p] : p;
+    if (!frozen[r]) m = (unsigned long long)(p - n_heavy + 1);
+  }
+  // (a wave's maximum, then one atomic per wave)
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long x = __shfl_xor(m, o);
+    m = x > m ? x : m;
+  }
+  if ((threadIdx.x & 63) == 0 && m) atomicMax(qlen, m);
 }
 
 // At most 128 VGPRs: a fill wave must fit beside the run kernel's wave in a
@@ -2967,6 +3074,11 @@ struct rwrt_ctx {
   int quad_per_wave = 16;      // latency mode: rays per wave (rwrt_ctx_set_latency_density)
   int64_t* trace = nullptr;    // rwrt_ctx_set_trace (diagnostic)
   int64_t trace_cap = 0;
+  int32_t slice_rows = 0;      // rwrt_ctx_set_slicing (0: off)
+  // sliced queue scratch: [0, 16) qlen (int64), then progress int32[slice_cap],
+  // then the hand-off records uint64[slice_cap][16] (128-B aligned)
+  char* slices = nullptr;
+  size_t slice_cap = 0;
   bool used = false;
   std::mutex mu;
 };
@@ -3001,6 +3113,24 @@ rwrt_status ctx_flags(rwrt_ctx* c, int64_t nray) {
   if (hipMalloc(reinterpret_cast<void**>(&c->flags), cap) != hipSuccess)
     return fail(RWRT_ERR_HIP, "frozen-ray flag allocation failed%s");
   c->cap = cap;
+  return RWRT_OK;
+}
+
+size_t slice_progress_bytes(size_t cap) { return (cap * sizeof(int32_t) + 127) & ~(size_t)127; }
+
+// Sliced-queue scratch for n queue positions (released like the flags).
+rwrt_status ctx_slices(rwrt_ctx* c, int64_t n) {
+  if ((size_t)n <= c->slice_cap && c->slices) return RWRT_OK;
+  if (c->slices) {
+    if ((c->used && hipEventSynchronize(c->done) != hipSuccess) || hipFree(c->slices) != hipSuccess)
+      return check_launch("releasing the context's slice scratch");
+    c->slices = nullptr;
+    c->slice_cap = 0;
+  }
+  const size_t cap = ((size_t)n + 4095) & ~(size_t)4095;
+  if (hipMalloc(reinterpret_cast<void**>(&c->slices), 128 + slice_progress_bytes(cap) + cap * 128) != hipSuccess)
+    return fail(RWRT_ERR_HIP, "slice scratch allocation failed%s");
+  c->slice_cap = cap;
   return RWRT_OK;
 }
 
@@ -3102,6 +3232,22 @@ rwrt_status launch_run(rwrt_ctx* ctx, const BG& B, int64_t nray, const rwrt_para
   // wait for a CU on its XCD until the persistent grid drains)
   a.heavy_blocks = (int32_t)team_blocks;
   a.quad_per_wave = quad_per_wave;
+  // row slicing: (queue position, slice) items over the positions live at the start
+  const int64_t rows = it_end - it_begin;
+  const int64_t nslices = ctx->slice_rows > 0 ? (rows + ctx->slice_rows - 1) / ctx->slice_rows : 1;
+  if (nslices > 1 && nray > n_heavy && nslices * (nray - n_heavy) < 0x7fffffffLL - (1LL << 24)) {
+    if (rwrt_status s = ctx_slices(ctx, nray - n_heavy)) return s;
+    a.slice_rows = ctx->slice_rows;
+    a.nslices = (int32_t)nslices;
+    a.qlen = reinterpret_cast<const int64_t*>(ctx->slices);
+    a.progress = reinterpret_cast<int32_t*>(ctx->slices + 128);
+    a.handoff = reinterpret_cast<uint64_t*>(ctx->slices + 128 + slice_progress_bytes(ctx->slice_cap));
+    if (hipMemsetAsync(ctx->slices, 0, 128 + (size_t)(nray - n_heavy) * sizeof(int32_t), st) != hipSuccess)
+      return check_launch("hipMemsetAsync(slice progress)");
+    hipLaunchKernelGGL(queue_extent_kernel, dim3(grid_for(nray - n_heavy, 256)), dim3(256), 0, st, d_order, nray,
+                       n_heavy, ctx->flags, reinterpret_cast<unsigned long long*>(ctx->slices));
+    if (rwrt_status s = check_launch("queue_extent_kernel")) return s;
+  }
   if constexpr (std::is_same<BG, StaticBG>::value) {
     a.trace = ctx->trace;
     a.trace_cap = ctx->trace ? ctx->trace_cap : 0;
@@ -3307,6 +3453,14 @@ rwrt_status rwrt_ctx_set_latency_density(rwrt_ctx* c, int32_t rays_per_wave) {
   return RWRT_OK;
 }
 
+rwrt_status rwrt_ctx_set_slicing(rwrt_ctx* c, int32_t slice_rows) {
+  if (!c) return fail(RWRT_ERR_ARG, "rwrt_ctx is NULL%s");
+  if (slice_rows < 0) return fail(RWRT_ERR_ARG, "slice_rows must be >= 0%s");
+  std::lock_guard<std::mutex> lock(c->mu);
+  c->slice_rows = slice_rows;
+  return RWRT_OK;
+}
+
 rwrt_status rwrt_ctx_set_trace(rwrt_ctx* c, int64_t* d_trace, int64_t capacity) {
   if (!c) return fail(RWRT_ERR_ARG, "rwrt_ctx is NULL%s");
   if (capacity < 0 || (capacity > 0 && !d_trace) || capacity > 0x7fffffffLL)
@@ -3326,6 +3480,7 @@ rwrt_status rwrt_ctx_destroy(rwrt_ctx* c) {
     // the last call's kernels may still read the flags / run on the side stream
     if (c->used && hipEventSynchronize(c->done) != hipSuccess) s = check_launch("rwrt_ctx_destroy");
     if (c->flags) (void)hipFree(c->flags);
+    if (c->slices) (void)hipFree(c->slices);
     if (c->side) (void)hipStreamDestroy(c->side);
     if (c->flagged) (void)hipEventDestroy(c->flagged);
     if (c->filled) (void)hipEventDestroy(c->filled);

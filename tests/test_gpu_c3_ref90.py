@@ -29,7 +29,7 @@ from make_devmath import row_hashes  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 
-def run_c3_90d(kind, team="auto"):
+def run_c3_90d(kind, team="auto", slice_rows=0):
     """Rows [7, 1081, n] and (nacc, nrej) of the fixture's sample, from a
     full-set 90-day run with the bench's schedule."""
     import torch
@@ -40,6 +40,7 @@ def run_c3_90d(kind, team="auto"):
     nt = int(g["nt"])
     bs, _ = make_bs(kind)
     eng = RayEngine.from_bs(bs)
+    eng.ctx.set_slicing(slice_rows)
     src, zcs = c3_sources(eng)
     rows0 = torch.cat([eng.initial_rows_dev(src, zc)[0].reshape(7, -1) for zc in zcs], dim=1)
     assert rows0.shape[1] == int(g["nslot"])
@@ -91,6 +92,15 @@ def test_c3_90d_sample_bitwise_with_reference_arithmetic(kind):
 
 def test_c3_90d_sample_latency_mode_bitwise():
     g, hist, counts = run_c3_90d("zonal", team=1024)
+    check(g, hist, counts)
+
+
+@pytest.mark.parametrize("kind", ["zonal", "nonzonal"])
+def test_c3_90d_sample_sliced_queue_bitwise(kind):
+    """The sliced work queue (rwrt_ctx_set_slicing, 7-row slices: a ray's 890-row
+    launch is 128 work items, its solver state handed between lanes, CUs and
+    XCDs 127 times) gives the same bits as one item per ray."""
+    g, hist, counts = run_c3_90d(kind, slice_rows=7)
     check(g, hist, counts)
 
 

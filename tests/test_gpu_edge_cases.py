@@ -163,3 +163,28 @@ def test_rk4_chunked_runs_equal_one_launch():
     with np.errstate(all="ignore"):
         href, _ = O.ray_run_rk4(O.Background(**bg), rows7[:5].copy(), nt, 7200.0, row0=rows7)
     assert _same(np.transpose(h2[:, 1:, :7], (2, 1, 0)), href[:, 1:])
+
+
+@pytest.mark.parametrize("n,slice_rows,team", [(129, 1, 0), (300, 5, 0), (1024, 3, 64), (4096, 10, 0)])
+def test_sliced_queue_bitwise(n, slice_rows, team):
+    """rwrt_ctx_set_slicing: every (ray, slice of ``slice_rows`` rows) is a work
+    item and the ray's solver state moves between lanes at slice ends; ragged
+    slice counts (24 rows in slices of 1, 3, 5, 10), rays that freeze in a
+    middle slice (their later slices skipped), dead slots, and the latency
+    mode beside it (the first ``team`` rays) -- bitwise the oracle's."""
+    eng, bg = _engine("nonzonal")
+    eng.ctx.set_slicing(slice_rows)
+    rows = golden("init_C2_nonzonal.npz")["rows"][:5].reshape(5, -1)
+    rng = np.random.default_rng(n)
+    pick = rng.choice(rows.shape[1], min(n, rows.shape[1]), replace=False)
+    y0 = np.ascontiguousarray(rows[:, pick])
+    out = {}
+    res = eng.integrate(torch.as_tensor(y0), NT, 7200.0, ttotal=(NT - 1) * 7200.0, chunk=24, team=team,
+                        sink=lambda a, b, o: out.__setitem__((a, b), o.cpu().numpy().copy()))
+    hist = np.full((y0.shape[1], NT, 8), np.nan)
+    for (i0, i1), r in out.items():
+        hist[:, i0:i1] = r
+    ref = _oracle(bg, y0, NT)
+    _check(hist, res, ref)
+    frozen_mid = np.isnan(ref[0][0, -1]) & ~np.isnan(ref[0][0, 1])
+    assert res.ray_steps > 0 and (n < 1024 or frozen_mid.any())

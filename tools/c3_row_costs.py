@@ -26,6 +26,11 @@ def main():
     ap.add_argument("--every", type=int, default=10)
     ap.add_argument("--out", default="/tmp/rwrt_rowcost")
     ap.add_argument("--features", default=None, help="directory for the compact per-live-ray feature file")
+    ap.add_argument("--compact", default=None,
+                    help="directory for c3_rowsub_<bg>.npz: a random 1/--sub of the live rays, "
+                         "running accepted steps as int16 (small enough for gpurun_out/)")
+    ap.add_argument("--sub", type=int, default=8)
+    ap.add_argument("--skip-full", action="store_true", help="only the --compact file")
     a = ap.parse_args()
     import torch
     from bench import c3_sources, make_bs
@@ -50,8 +55,17 @@ def main():
                         sink=sink, ttotal=(nt - 1) * 7200.0, team="auto")
         nacc = torch.cat(cols, dim=1).numpy()
         att = r.counts.sum(1).to(torch.int32).cpu().numpy()
-        np.savez_compressed(os.path.join(a.out, f"c3_rowcost_{kind}.npz"), rows=np.array(rows), nacc=nacc,
-                            att=att, bounds=np.array([[1, 7]] + [list(b) for b in r.res.bounds]))
+        bounds = np.array([[1, 7]] + [list(b) for b in r.res.bounds])
+        if not a.skip_full:
+            np.savez_compressed(os.path.join(a.out, f"c3_rowcost_{kind}.npz"), rows=np.array(rows), nacc=nacc,
+                                att=att, bounds=bounds)
+        if a.compact:
+            os.makedirs(a.compact, exist_ok=True)
+            live = np.nonzero(att > 0)[0]
+            sub = np.sort(np.random.default_rng(1).choice(live, size=len(live) // a.sub, replace=False))
+            np.savez_compressed(os.path.join(a.compact, f"c3_rowsub_{kind}.npz"), rows=np.array(rows),
+                                nacc=np.minimum(nacc[sub], 32767).astype(np.int16), att=att[sub],
+                                slot=sub.astype(np.int32), n_live=len(live), sub=a.sub, bounds=bounds)
         if a.features:
             # a compact per-live-ray feature set for studying cost predictors
             live = np.nonzero(att > 0)[0]
