@@ -311,8 +311,10 @@ def main():
     ap.add_argument("--split", default="auto", choices=["auto", "off"],
                     help="split the long launch once more when the leading launches' per-ray work "
                          "predicts the next poorly (RayEngine.SPLIT_RHO)")
-    ap.add_argument("--slice", type=int, default=0,
-                    help="rows per work item of the ray loop's queue (rwrt_ctx_set_slicing; 0: one item per ray)")
+    ap.add_argument("--phases", default=None,
+                    help="C3: run the rows after the probe in scheduling phases (RayEngine.advance_budgeted) "
+                         "with these comma-separated row targets ('default': RayEngine.PHASE_TARGETS; "
+                         "'off': row launches)")
     ap.add_argument("--team", default="auto",
                     help="rays per launch in latency mode (quad_rays: four lanes of a wave per ray); "
                          "an integer or 'auto' (RayEngine.team_size)")
@@ -385,7 +387,6 @@ def main():
     if args.replicate > 1:
         y0 = np.concatenate([y0] * args.replicate, axis=1)
     eng = RayEngine.from_bs(bs, device=dev)
-    eng.ctx.set_slicing(args.slice)
     nt = int(round(args.days * 12)) + 1
     gpu_init = args.replicate == 1
     init_same = None
@@ -420,6 +421,10 @@ def main():
     lead = [int(x) for x in str(args.first_chunk).split(",") if x]
     team = args.team if args.team == "auto" else int(args.team)
     split = None if args.split == "off" else args.split
+    phases = (None if args.phases in (None, "off")
+              else [] if args.phases == "default"
+              else {"budgets": [1e3 * float(x) for x in args.phases[2:].split(",")]} if args.phases.startswith("t:")
+              else [int(x) for x in str(args.phases).split(",") if x])
     gather_dev = torch.device("cpu") if backend == "gloo" else dev
     n_live_max = n_live
     if weak and dist:
@@ -450,12 +455,12 @@ def main():
         if weak:
             r = run_sharded(eng, y, nt, 7200.0, rank=0, world=1, probe=args.probe, lead=lead,
                             chunk=chunk, out=out, events=events, ttotal=(nt - 1) * 7200.0,
-                            order_policy=args.order, team=team, split=split)
+                            order_policy=args.order, team=team, split=split, phases=phases)
             gather_endpoints(r)
             return r
         return run_sharded(eng, y, nt, 7200.0, group=group, probe=args.probe, lead=lead,
                            chunk=chunk, out=out, events=events, ttotal=(nt - 1) * 7200.0,
-                           order_policy=args.order, team=team, split=split)
+                           order_policy=args.order, team=team, split=split, phases=phases)
 
     for _ in range(args.warmup):
         one_step()
@@ -497,7 +502,8 @@ def main():
                     + (" (BASELINE configs[2])" if world == 1 else
                        (" per GPU, the seed grid shifted by rank x 2/N deg of longitude (BASELINE configs[3], "
                         "weak scaling)" if weak else " (BASELINE configs[3]: C4, one set split)")))
-        schedule = [args.probe] + [b - a for a, b in r.res.bounds]
+        schedule = ([args.probe] + [b - a for a, b in r.res.bounds] if phases is None
+                    else [args.probe, r.res.bounds[-1][1] - r.res.bounds[0][0]])
         if weak:
             par = (f"{world} rank(s), one GPU each (backend {backend or 'none'}): each integrates its own "
                    f"C3 seed grid (2.40 M slots), no exchange during integration; inside the timed step "
@@ -516,7 +522,9 @@ def main():
             "config": {"workload": workload,
                        "ray_slots": nslot * (world if weak else 1), "live_rays_rank0": n_live,
                        "rows": nt, "rows_per_launch": chunk, "launch_rows": schedule,
-                       "slice_rows": args.slice,
+                       "phases": (None if phases is None else
+                                  {"row_targets": [b for a, b in r.res.bounds],
+                                   "grace_us": eng.GRACE_US, "spec": args.phases}),
                        "rank0_rays": n_mine,
                        "latency_mode": ("per launch, the heaviest rays whose move to quad_rays (four lanes of a "
                                         "wave per ray) minimises the predicted makespan by >= 10 %"
@@ -651,7 +659,6 @@ def main_c5(args, dist, group, rank, world, dev, share=1):
     torch.cuda.synchronize()
     t_build = time.perf_counter() - t_build
     eng = RayEngine.from_levels(lv)
-    eng.ctx.set_slicing(args.slice)
     cfg = S.config("C5")
     deg2rad = np.pi / 180.0
     ix, iy = np.meshgrid(np.arange(cfg.nnx), np.arange(cfg.nny))
@@ -741,7 +748,7 @@ def main_c5(args, dist, group, rank, world, dev, share=1):
             "config": {"workload": workload, "ray_slots": nslot, "live_rays": n_live,
                        "rows": nt, "levels": nlev, "field_storage": args.fields,
                        "level_bytes": int(lv.packed[0].numel() * lv.packed.element_size()),
-                       "rows_per_launch": chunk, "launch_rows": schedule, "slice_rows": args.slice,
+                       "rows_per_launch": chunk, "launch_rows": schedule,
                        "parallelism": (f"{world} rank(s), each its own C5 seed grid (shifted by rank/N deg)"
                                        if weak else f"one ray set over {world} GPU(s) (run_sharded, as C3/C4)")},
             "parity_sample_vs_oracle": parity,

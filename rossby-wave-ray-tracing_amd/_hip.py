@@ -14,10 +14,10 @@ LIB_PATH = os.environ.get("RWRT_LIB", os.path.join(_HERE, "librwrt.so"))
 
 NFIELD_REF, NFIELD_PACK, NVAR, NMERC, NOUT, NSTATE = 18, 12, 5, 12, 8, 12
 ABI_SYMBOLS = ("rwrt_version", "rwrt_last_error", "rwrt_ctx_create", "rwrt_ctx_destroy",
-               "rwrt_ctx_set_latency_density", "rwrt_ctx_set_trace", "rwrt_ctx_set_slicing",
+               "rwrt_ctx_set_latency_density", "rwrt_ctx_set_trace",
                "rwrt_pack_fields",
                "rwrt_mercator_point", "rwrt_rhs", "rwrt_dp54_attempt",
-               "rwrt_ray_initial", "rwrt_rk45_init", "rwrt_rk45_run", "rwrt_rk4_run",
+               "rwrt_ray_initial", "rwrt_rk45_init", "rwrt_rk45_run", "rwrt_rk45_run_budget", "rwrt_rk4_run",
                "rwrt_bs_ready", "rwrt_rk45_init_tv", "rwrt_rk45_run_tv", "rwrt_rhs_tv",
                "rwrt_kat_rk45", "rwrt_selftest_math", "rwrt_host_fill_rows")
 
@@ -77,6 +77,8 @@ def load():
         "rwrt_ray_initial": [G, _P, _I64, _P, _P, _P, _I32, _P, _P, _P, _P],
         "rwrt_rk45_init": [G, _P, _I64, _P, Pr, _P, _P, _P, _P, _P, _P],
         "rwrt_rk45_run": [_P, G, _P, _I64, Pr, _P, _I32, _I32, _P, _I64, _P, _P, _P, _P, _P, _P],
+        "rwrt_rk45_run_budget": [_P, G, _P, _I64, Pr, _P, _I32, _I32, _P, _I64, _P, _P, _P, _P, _P, _P,
+                                 _I32, _P, _D, _D, _P],
         "rwrt_rk4_run": [_P, G, _P, _I64, Pr, _I32, _I32, _P, _P, _P, _P, _P, _P, _P],
         "rwrt_bs_ready": [_I32, _I32, _P, _P, _P, _D, _D, _P, _P, _I32, _P],
         "rwrt_rk45_init_tv": [G, B, _I64, _P, Pr, _P, _P, _P, _P, _P, _P],
@@ -85,7 +87,6 @@ def load():
         "rwrt_ctx_destroy": [_P],
         "rwrt_ctx_set_latency_density": [_P, _I32],
         "rwrt_ctx_set_trace": [_P, _P, _I64],
-        "rwrt_ctx_set_slicing": [_P, _I32],
         "rwrt_rhs_tv": [G, B, _I64, _P, _P, _P, _P],
         "rwrt_kat_rk45": [_I32, _I64, _P, _I32, _P, _D, _D, _D, _P, _P],
         "rwrt_selftest_math": [_I32, _I64, _P, _P, _P, _P],
@@ -156,13 +157,6 @@ class Context:
         if getattr(self, "_qpw", 16) != int(rays_per_wave):
             check(load().rwrt_ctx_set_latency_density(self._h, int(rays_per_wave)))
             self._qpw = int(rays_per_wave)
-
-    def set_slicing(self, slice_rows):
-        """Rows per work item of the ray loop's queue (0: one item per ray):
-        rwrt_ctx_set_slicing.  Schedule only."""
-        if getattr(self, "_slice", 0) != int(slice_rows):
-            check(load().rwrt_ctx_set_slicing(self._h, int(slice_rows)))
-            self._slice = int(slice_rows)
 
     def set_trace(self, trace=None):
         """Diagnostic ray trace (rwrt_ctx_set_trace): ``trace`` an int64 device

@@ -1835,35 +1835,39 @@ struct RunArgs {
   int32_t quad_per_wave = 16;  // latency mode: rays per wave (1..16; fewer = less divergence per ray)
   int64_t* trace = nullptr;    // diagnostic ray trace (rwrt_ctx_set_trace), positions < trace_cap
   int64_t trace_cap = 0;
-  // row slicing (rwrt_ctx_set_slicing): work items (queue position, slice)
-  int32_t slice_rows = 0;      // 0: one item per ray, rows [it_begin, it_end)
-  int32_t nslices = 1;
-  const int64_t* qlen = nullptr;   // [1] queued positions that hold a ray live at the start (queue_extent_kernel)
-  int32_t* progress = nullptr;     // [qlen] slices ended per position (kSliceFrozen: frozen, rows written)
-  uint64_t* handoff = nullptr;     // [qlen][16] the ray's solver state between its slices
+  // budgeted calls (rwrt_rk45_run_budget): each ray continues from rowpos[ray]
+  // and, once `budget` ticks of s_memrealtime (100 MHz) have passed since its
+  // wave started, stops at its next output row and records it there
+  int32_t* rowpos = nullptr;   // NULL: every ray runs rows [it_begin, it_end)
+  double* prev = nullptr;      // [2][nray] lon, lat of the row before rowpos (the jump mask's reference)
+  uint64_t budget = 0;         // 0: no deadline
+  uint64_t grace = ~0ull;      // stop this long after the queue has drained (~0: never)
+  const int64_t* qlen = nullptr;  // queue positions after n_heavy that can hold work (queue_extent_kernel)
+  int32_t out_nrows = 0;       // rows per ray of d_out (which starts at row it_begin)
 };
 
-// Sliced work queue (rwrt_ctx_set_slicing).  A ray's state moves between the
-// lanes that run its slices through one 128-B record per queue position:
-// words 0-4 y, 5-9 f, 10 t, 11 h_abs, 12 accepted, 13 rejected, 14 nanrow.
-// Every access to the records and to the progress words inside the launch is
-// agent-coherent (sc1: __hip_atomic_* relaxed, agent scope); the lane that
-// ends a slice waits for its record stores (vmcnt(0)) before it publishes the
-// slice's end (MI355X_MICROARCH.md, inter-workgroup visibility: sc1 payload,
-// drained, then an sc1 flag; the consumer polls sc1 and loads sc1).
-constexpr int32_t kSliceFrozen = 0x7fffffff;
-__device__ __forceinline__ void hand_put(uint64_t* rec, int j, uint64_t v) {
-  __hip_atomic_store(rec + j, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint64_t hand_get(const uint64_t* rec, int j) {
-  return __hip_atomic_load(const_cast<uint64_t*>(rec) + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void hand_putd(uint64_t* rec, int j, double v) { hand_put(rec, j, (uint64_t)__double_as_longlong(v)); }
-__device__ __forceinline__ double hand_getd(const uint64_t* rec, int j) { return __longlong_as_double((long long)hand_get(rec, j)); }
-__device__ __forceinline__ void slice_publish(int32_t* progress, int64_t q, int32_t v) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the record's stores have completed
-  __hip_atomic_store(progress + q, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
+// Wave-uniform end of a budgeted call: `budget` ticks after the wave started,
+// or `grace` ticks after the wave first saw the work queue drained -- the
+// real-time counter (and the queue head) read every 32nd iteration of the ray
+// loop (~0.4 ms of a wave)
+struct Deadline {
+  uint64_t at = ~0ull;
+  uint32_t tick = 0;
+  bool passed = false, armed = false;
+  __device__ __forceinline__ Deadline(uint64_t budget, uint64_t grace) {
+    armed = budget || grace != ~0ull;
+    if (budget) at = __builtin_amdgcn_s_memrealtime() + budget;
+  }
+  template <class A>
+  __device__ __forceinline__ void poll(const A& a, int64_t qend) {
+    if (!armed || passed || (++tick & 31u) != 0) return;
+    const uint64_t now = __builtin_amdgcn_s_memrealtime();
+    if (a.grace != ~0ull && at - now > a.grace &&
+        a.n_heavy + __hip_atomic_load(&a.queue[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= qend)
+      at = now + a.grace;   // the queue has drained: the stragglers stop soon
+    passed = now >= at;
+  }
+};
 
 // rwrt_ctx_set_trace: where (HW_ID, XCC) and when a traced ray ran
 constexpr int kTraceWords = 10;
@@ -2170,7 +2174,6 @@ __device__ __forceinline__ void quad_rays(const RunArgs<StaticBG>& a, char* cach
   R.odd = (R.role & 1) != 0;
   R.high = (R.role & 2) != 0;
   KQuad K{Kq + threadIdx.x};
-  const int64_t nrows = a.it_end - a.it_begin;
   // order position of this quad's ray: the heaviest rays one per wave first
   // (position p -> wave p % waves, quad p / waves), a.quad_per_wave quads per wave
   const int qi = (threadIdx.x & 63) >> 2;
@@ -2193,12 +2196,17 @@ __device__ __forceinline__ void quad_rays(const RunArgs<StaticBG>& a, char* cach
   const int64_t att0 = nacc + nrej;
   if (kTrace && w < a.trace_cap && R.role == 0) trace_start(a.trace, w);
   int32_t nanrow = a.nanrow[ray];
-  int32_t it = a.it_begin;
-  double prev_lon = y[0], prev_lat = y[1], cos_prev = k_cos(prev_lat);
+  int32_t it = a.rowpos ? a.rowpos[ray] : a.it_begin;
+  if (it >= a.it_end) return;   // (budgeted calls: done in an earlier one)
+  double prev_lon = a.prev ? a.prev[ray] : y[0], prev_lat = a.prev ? a.prev[a.nray + ray] : y[1];
+  double cos_prev = k_cos(prev_lat);
   aux[2] = kNaN;
   bool in_step = false, rejected = false;
   const bool writer = R.role == 0;
+  const int64_t qend = a.n_heavy + (a.qlen ? *a.qlen : a.nray - a.n_heavy);
+  Deadline dl(a.budget, a.grace);
   for (;;) {
+    dl.poll(a, qend);
     const double tb = a.tbound[it];
     // ---- Lane::iterate (rkf45.py:222-253, 375-514)
     int st = 0;   // 0 step, 1 reached, 2 frozen
@@ -2241,7 +2249,10 @@ __device__ __forceinline__ void quad_rays(const RunArgs<StaticBG>& a, char* cach
       rejected = rejected || !acc;
       nacc += acc ? 1 : 0;
       nrej += acc ? 0 : 1;
-      if (!(acc && t - tb >= 0.0)) continue;
+      if (!(acc && t - tb >= 0.0)) {
+        if (dl.passed && acc) break;   // (budgeted: stop inside row it after an accepted step)
+        continue;
+      }
       st = 1;
     }
     // ---- interval it reached: rk45_run_kernel's post-processing (wr.py:835-885)
@@ -2269,7 +2280,7 @@ __device__ __forceinline__ void quad_rays(const RunArgs<StaticBG>& a, char* cach
       const double2 r0 = make_double2(y[0], y[1]), r1 = make_double2(y[2], y[3]);
       const double2 r2 = make_double2(y[4], ug), r3 = make_double2(vg, (double)nacc);
       for (int kr = it; kr < last; ++kr) {
-        double2* o = reinterpret_cast<double2*>(a.out + ((size_t)ray * nrows + (kr - a.it_begin)) * RWRT_NOUT);
+        double2* o = reinterpret_cast<double2*>(a.out + ((size_t)ray * a.out_nrows + (kr - a.it_begin)) * RWRT_NOUT);
         o[0] = r0;
         o[1] = r1;
         o[2] = r2;
@@ -2282,9 +2293,14 @@ __device__ __forceinline__ void quad_rays(const RunArgs<StaticBG>& a, char* cach
     cos_prev = cos_c;
     it = last;
     if (st == 2) t = a.tbound[a.it_end - 1];
-    if (it == a.it_end) break;
+    if (it == a.it_end || dl.passed) break;
   }
   if (writer) {
+    if (a.rowpos) {
+      a.rowpos[ray] = it;
+      a.prev[ray] = prev_lon;
+      a.prev[a.nray + ray] = prev_lat;
+    }
 #pragma unroll
     for (int v = 0; v < 5; ++v) {
       a.state[v * a.nray + ray] = y[v];
@@ -2308,6 +2324,29 @@ __device__ __forceinline__ void quad_rays(const RunArgs<StaticBG>& a, char* cach
 // latency mode (quad_rays in the grid's first blocks, order[0, n_heavy)); the
 // queue is the rest.
 using KStore = KShared<5>;
+
+// A ray leaves its lane: its solver state (and, in budgeted calls, the row it
+// is in and that row's reference position) back to the per-ray arrays
+template <class A>
+__device__ __forceinline__ void retire_ray(const A& a, int64_t ray, int32_t it, const double* y, const double* f,
+                                           double t, double habs, int64_t nacc, int64_t nrej, int32_t nanrow,
+                                           double prev_lon, double prev_lat) {
+#pragma unroll
+  for (int v = 0; v < 5; ++v) {
+    a.state[v * a.nray + ray] = y[v];
+    a.state[(5 + v) * a.nray + ray] = f[v];
+  }
+  a.state[10 * a.nray + ray] = t;
+  a.state[11 * a.nray + ray] = habs;
+  a.count[2 * ray] = nacc;
+  a.count[2 * ray + 1] = nrej;
+  a.nanrow[ray] = nanrow;
+  if (a.rowpos) {
+    a.rowpos[ray] = it;
+    a.prev[ray] = prev_lon;
+    a.prev[a.nray + ray] = prev_lat;
+  }
+}
 // kTrace: the diagnostic instantiation (rwrt_ctx_set_trace) -- the product
 // kernel carries none of the trace hooks
 template <class BG, bool kTrace = false>
@@ -2326,94 +2365,73 @@ __global__ void __launch_bounds__(256, 1) rk45_run_kernel(RunArgs<BG> a) {
     }
   }
   const RayProblem P{LaneBG<BG>::make(a.B, smem + kKBytes)};
-  const int64_t nrows = a.it_end - a.it_begin;
   Lane<RayProblem, KStore> L;
   L.K.p = reinterpret_cast<double*>(smem) + threadIdx.x;
   L.K.stride = 256;
   int64_t ray = -1, nacc = 0, nrej = 0;
   int32_t it = 0, nanrow = 0, wpos = 0;   // (wpos: the ray's queue position, kTrace only)
   double prev_lon = 0.0, prev_lat = 0.0, cos_prev = 0.0;
-  // work items: one per queued ray, or (rwrt_ctx_set_slicing) one per (queue
-  // position, slice): slice 0 of every position in the order, then slice 1, ...
-  const bool sliced = a.slice_rows > 0;
-  const int64_t nq = sliced ? *a.qlen : a.nray - a.n_heavy;
-  const int64_t n_items = sliced ? nq * a.nslices : nq;
-  int64_t pend = -1, qpos = 0;   // pend: an item claimed while its ray's previous slice still runs
-  int32_t it_stop = a.it_end;
   if (1) {
     // above frozen_fill_kernel's waves (priority 0) sharing the SIMD: the
     // fill takes the issue cycles the ray loop leaves idle
     __builtin_amdgcn_s_setprio(1);
   }
+  const int64_t qend = a.n_heavy + (a.qlen ? *a.qlen : a.nray - a.n_heavy);
+  Deadline dl(a.budget, a.grace);
   for (;;) {
+    dl.poll(a, qend);
     if (ray < 0) {
-      int64_t c = pend;
-      if (c < 0) {
-        c = atomicAdd(&a.queue[1], 1);
-        if (c >= n_items) break;
-      }
-      pend = -1;
-      int32_t k = 0;
-      int64_t q = c;
-      if (sliced) {
-        k = (int32_t)(c / nq);
-        q = c - (int64_t)k * nq;
-      }
-      const int64_t w = a.n_heavy + q;
-      const int64_t r = a.order ? a.order[w] : w;
+      if (dl.passed) break;
+      const int64_t w = a.n_heavy + atomicAdd(&a.queue[1], 1);
+      if (w >= qend) break;
+      ray = a.order ? a.order[w] : w;
       if (kTrace) {
         wpos = (int32_t)w;
-        if (k == 0 && w < a.trace_cap) trace_start(a.trace, w);
+        if (w < a.trace_cap) trace_start(a.trace, w);
       }
-      if (a.frozen && a.frozen[r]) continue;   // its rows come from frozen_fill_kernel
-      if (k > 0) {
-        const int32_t done = __hip_atomic_load(a.progress + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (done == kSliceFrozen) continue;    // frozen in an earlier slice: its rows are written
-        if (done < k) {                        // the previous slice still runs: look again next iteration
-          pend = c;
-          continue;
-        }
+      if (a.frozen && a.frozen[ray]) {   // its rows come from frozen_fill_kernel
+        ray = -1;
+        continue;
       }
-      ray = r;
-      qpos = q;
-      it = a.it_begin + k * a.slice_rows;
-      it_stop = sliced ? min(it + a.slice_rows, a.it_end) : a.it_end;
-      if (k == 0) {
+      it = a.rowpos ? a.rowpos[ray] : a.it_begin;
+      if (it >= a.it_end) {   // (budgeted calls: done in an earlier one)
+        ray = -1;
+        continue;
+      }
 #pragma unroll
-        for (int v = 0; v < 5; ++v) {
-          L.y[v] = a.state[v * a.nray + ray];
-          L.f[v] = a.state[(5 + v) * a.nray + ray];
-        }
-        L.t = a.state[10 * a.nray + ray];
-        L.habs = a.state[11 * a.nray + ray];
-        nacc = a.count[2 * ray];
-        nrej = a.count[2 * ray + 1];
-        nanrow = a.nanrow[ray];
-      } else {
-        asm volatile("");   // (a ray's later slice: its state from the hand-off record)
-        const uint64_t* rec = a.handoff + q * 16;
-#pragma unroll
-        for (int v = 0; v < 5; ++v) {
-          L.y[v] = hand_getd(rec, v);
-          L.f[v] = hand_getd(rec, 5 + v);
-        }
-        L.t = hand_getd(rec, 10);
-        L.habs = hand_getd(rec, 11);
-        nacc = (int64_t)hand_get(rec, 12);
-        nrej = (int64_t)hand_get(rec, 13);
-        nanrow = (int32_t)hand_get(rec, 14);
+      for (int v = 0; v < 5; ++v) {
+        L.y[v] = a.state[v * a.nray + ray];
+        L.f[v] = a.state[(5 + v) * a.nray + ray];
       }
+      L.t = a.state[10 * a.nray + ray];
+      L.habs = a.state[11 * a.nray + ray];
       L.in_step = false;
       L.rejected = false;
       L.hs = 0.0;
+      nacc = a.count[2 * ray];
+      nrej = a.count[2 * ray + 1];
+      nanrow = a.nanrow[ray];
       prev_lon = L.y[0];   // == rlon[it-1], rlat[it-1] (wr.py:844, 877-885)
       prev_lat = L.y[1];
+      if (a.prev) {        // (budgeted calls: the ray may have stopped inside row it)
+        prev_lon = a.prev[ray];
+        prev_lat = a.prev[a.nray + ray];
+      }
       cos_prev = k_cos(prev_lat);
       L.aux[2] = kNaN;     // no evaluation at y yet
     }
     const double tb = a.tbound[it];
     const int st = L.iterate(P, tb, a.min_step, a.rtol, a.atol, nacc, nrej);
-    if (st == Lane<RayProblem, KStore>::kStep) continue;
+    if (st == Lane<RayProblem, KStore>::kStep) {
+      // (budgeted calls past their end: stop inside row it after an accepted
+      // step -- the loop state is then y, f, t, h_abs and the row's reference
+      // position, as after any accepted step)
+      if (!(dl.passed && !L.in_step)) continue;
+      asm volatile("");
+      retire_ray(a, ray, it, L.y, L.f, L.t, L.habs, nacc, nrej, nanrow, prev_lon, prev_lat);
+      ray = -1;
+      continue;
+    }
 
     // ---- interval it reached: post-processing (wr.py:835-885) ----
     // The last accepted step's K6 evaluation was at this y: its cos(lat), ug
@@ -2449,7 +2467,7 @@ __global__ void __launch_bounds__(256, 1) rk45_run_kernel(RunArgs<BG> a) {
     // equals this one: write them all and release the lane.
     const int last = (st == Lane<RayProblem, KStore>::kFrozen) ? a.it_end : it + 1;
     if (!0) {   // (timing-only diagnostic build: no row stores)
-      double2* o = reinterpret_cast<double2*>(a.out + ((size_t)ray * nrows + (it - a.it_begin)) * RWRT_NOUT);
+      double2* o = reinterpret_cast<double2*>(a.out + ((size_t)ray * a.out_nrows + (it - a.it_begin)) * RWRT_NOUT);
       store_row16<0>(o + 0, r0);
       store_row16<0>(o + 1, r1);
       store_row16<0>(o + 2, r2);
@@ -2458,7 +2476,7 @@ __global__ void __launch_bounds__(256, 1) rk45_run_kernel(RunArgs<BG> a) {
     if (!0 && last > it + 1) {
       asm volatile("");   // frozen: the remaining rows of the chunk (rare branch)
       for (int k = it + 1; k < last; ++k) {
-        double2* o = reinterpret_cast<double2*>(a.out + ((size_t)ray * nrows + (k - a.it_begin)) * RWRT_NOUT);
+        double2* o = reinterpret_cast<double2*>(a.out + ((size_t)ray * a.out_nrows + (k - a.it_begin)) * RWRT_NOUT);
         o[0] = r0;
         o[1] = r1;
         o[2] = r2;
@@ -2471,36 +2489,10 @@ __global__ void __launch_bounds__(256, 1) rk45_run_kernel(RunArgs<BG> a) {
     cos_prev = cos_c;
     it = last;
     if (st == Lane<RayProblem, KStore>::kFrozen) L.t = a.tbound[a.it_end - 1];
-    if (it == a.it_end) {
-#pragma unroll
-      for (int v = 0; v < 5; ++v) {
-        a.state[v * a.nray + ray] = y[v];
-        a.state[(5 + v) * a.nray + ray] = L.f[v];
-      }
-      a.state[10 * a.nray + ray] = L.t;
-      a.state[11 * a.nray + ray] = L.habs;
+    if (it == a.it_end || dl.passed) {   // the call's end, or its deadline at this row
       if (kTrace && wpos < a.trace_cap)
         trace_ray(a.trace, wpos, ray, nacc + nrej - a.count[2 * ray] - a.count[2 * ray + 1], false);
-      a.count[2 * ray] = nacc;
-      a.count[2 * ray + 1] = nrej;
-      a.nanrow[ray] = nanrow;
-      // frozen before the last slice: its later slices are skipped
-      if (sliced && it_stop < a.it_end) slice_publish(a.progress, qpos, kSliceFrozen);
-      ray = -1;
-    } else if (it == it_stop) {
-      asm volatile("");   // (sliced: the end of one of the ray's slices, not the call's)
-      uint64_t* rec = a.handoff + qpos * 16;
-#pragma unroll
-      for (int v = 0; v < 5; ++v) {
-        hand_putd(rec, v, y[v]);
-        hand_putd(rec, 5 + v, L.f[v]);
-      }
-      hand_putd(rec, 10, L.t);
-      hand_putd(rec, 11, L.habs);
-      hand_put(rec, 12, (uint64_t)nacc);
-      hand_put(rec, 13, (uint64_t)nrej);
-      hand_put(rec, 14, (uint64_t)(int64_t)nanrow);
-      slice_publish(a.progress, qpos, (it - a.it_begin) / a.slice_rows);
+      retire_ray(a, ray, it, y, L.f, L.t, L.habs, nacc, nrej, nanrow, prev_lon, prev_lat);
       ray = -1;
     }
   }
@@ -2529,21 +2521,20 @@ __global__ void frozen_flag_kernel(const double* __restrict__ state, int64_t nra
   }
 }
 
-// Sliced queue (rwrt_ctx_set_slicing): the queue positions that hold a ray
-// live at the call's start end at qlen[0] -- one past the last such position
-// of the order after the latency-mode entries (any order; the engine's put
-// the frozen rays last), so that a round of slices does not walk the frozen
-// rays (70 % of C3's slots).  qlen[0] is zeroed before.
+// The queue's end: one past the last position (after the latency-mode
+// entries) whose ray has work in the call -- live at its start and, in a
+// budgeted call, not yet at it_end -- so that lanes do not walk the frozen and
+// finished rays the engine's orders put last (70 % of C3's slots).
 __global__ void queue_extent_kernel(const int64_t* __restrict__ order, int64_t nray, int64_t n_heavy,
-                                    const uint8_t* __restrict__ frozen, unsigned long long* __restrict__ qlen) {
+                                    const uint8_t* __restrict__ frozen, const int32_t* __restrict__ rowpos,
+                                    int32_t it_end, unsigned long long* __restrict__ qlen) {
   unsigned long long m = 0;
   for (int64_t p = n_heavy + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < nray;
        p += (int64_t)gridDim.x * blockDim.x) {
     const int64_t r = order ? order[p] : p;
-    if (!frozen[r]) m = (unsigned long long)(p - n_heavy + 1);
+    if (!frozen[r] && (!rowpos || rowpos[r] < it_end)) m = (unsigned long long)(p - n_heavy + 1);
   }
-  // (a wave's maximum, then one atomic per wave)
-  for (int o = 32; o > 0; o >>= 1) {
+  for (int o = 32; o > 0; o >>= 1) {   // the wave's maximum, then one atomic per wave
     const unsigned long long x = __shfl_xor(m, o);
     m = x > m ? x : m;
   }
@@ -2560,14 +2551,16 @@ constexpr int kFillThreads = 64;
 // ray's rows are); thread t stores quarter t & 3 of the 64-B row, read from
 // the ray's lane by cross-lane reads -- no LDS, so that a fill wave fits
 // beside rk45_run_kernel's 155 KB block on every CU.
-__device__ __forceinline__ void write_frozen_tile(double* out, int64_t base, int64_t nrows, bool mine,
-                                                  double2 r0, double2 r1, double2 r2, double2 r3) {
+__device__ __forceinline__ void write_frozen_tile(double* out, int64_t base, int64_t nrows, int64_t last,
+                                                  bool mine, int32_t first, double2 r0, double2 r1, double2 r2,
+                                                  double2 r3) {
   unsigned long long lanes = __ballot(mine);
-  const int64_t nq = nrows * 4;
+  const int64_t nq = last * 4;   // rows [first, last) of each ray's nrows
   const int qt = threadIdx.x & 3;
   while (lanes) {
     const int j = __builtin_ctzll(lanes);
     lanes &= lanes - 1;
+    const int64_t qfirst = 4 * (int64_t)__shfl(first, j);   // the ray's first row of the call (rowpos)
     double2* o = reinterpret_cast<double2*>(out + (size_t)(base + j) * nrows * RWRT_NOUT);
     // (every lane reads lane j's quarters 0..3 in turn and keeps its own)
     const double2 q0 = make_double2(__shfl(r0.x, j), __shfl(r0.y, j));
@@ -2575,11 +2568,11 @@ __device__ __forceinline__ void write_frozen_tile(double* out, int64_t base, int
     const double2 q2 = make_double2(__shfl(r2.x, j), __shfl(r2.y, j));
     const double2 q3 = make_double2(__shfl(r3.x, j), __shfl(r3.y, j));
     const double2 v = qt == 0 ? q0 : qt == 1 ? q1 : qt == 2 ? q2 : q3;
-    for (int64_t q = threadIdx.x; q < nq; q += kFillThreads) store_row16<1>(o + q, v);
+    for (int64_t q = qfirst + threadIdx.x; q < nq; q += kFillThreads) store_row16<1>(o + q, v);
     // pace the stores (~0.9 us per full 64 rows written; none for shorter
     // chunks): a full-rate fill floods the memory queues the run kernel's
     // lookups wait in
-    for (int64_t z = 64; z <= nrows; z += 64) __builtin_amdgcn_s_sleep(32);
+    for (int64_t z = 64; z <= last - qfirst / 4; z += 64) __builtin_amdgcn_s_sleep(32);
   }
 }
 
@@ -2587,10 +2580,12 @@ template <class BG>
 __global__ void __launch_bounds__(kFillThreads) __attribute__((amdgpu_num_vgpr(128)))
 frozen_fill_kernel(RunArgs<BG> a) {
   nm_stage<NM_SINCOS>();
-  const int64_t nrows = a.it_end - a.it_begin;
   const int64_t base = blockIdx.x * (int64_t)kFillThreads;
   const int64_t ray = base + threadIdx.x;
-  const bool mine = ray < a.nray && a.frozen[ray];
+  // (budgeted calls: a ray frozen in an earlier call of the row range wrote
+  // its rows to it_end there; rowpos = it_end)
+  const int32_t it = (ray < a.nray && a.rowpos) ? a.rowpos[ray] : a.it_begin;
+  const bool mine = ray < a.nray && a.frozen[ray] && it < a.it_end;
   double2 r0 = make_double2(0.0, 0.0), r1 = r0, r2 = r0, r3 = r0;
   if (mine) {
     // rk45_run_kernel's fetch + kFrozen iteration + post-processing, verbatim
@@ -2599,7 +2594,6 @@ frozen_fill_kernel(RunArgs<BG> a) {
     for (int v = 0; v < 5; ++v) y[v] = a.state[v * a.nray + ray];
     const int64_t nacc = a.count[2 * ray];
     int32_t nanrow = a.nanrow[ray];
-    const int32_t it = a.it_begin;
     const double prev_lon = y[0], prev_lat = y[1];
     const double cos_prev = k_cos(prev_lat);
     const double tb = a.tbound[it];
@@ -2625,8 +2619,9 @@ frozen_fill_kernel(RunArgs<BG> a) {
     for (int v = 0; v < 5; ++v) a.state[v * a.nray + ray] = y[v];
     a.state[10 * a.nray + ray] = a.tbound[a.it_end - 1];
     a.nanrow[ray] = nanrow;
+    if (a.rowpos) a.rowpos[ray] = a.it_end;
   }
-  write_frozen_tile(a.out, base, nrows, mine, r0, r1, r2, r3);
+  write_frozen_tile(a.out, base, a.out_nrows, a.it_end - a.it_begin, mine, it - a.it_begin, r0, r1, r2, r3);
 }
 
 
@@ -2846,7 +2841,7 @@ rk4_fill_kernel(Rk4Args a) {
     a.count[2 * ray] = nstep;
     a.nanrow[ray] = nanrow;
   }
-  write_frozen_tile(a.out, base, nrows, mine, r0, r1, r2, r3);
+  write_frozen_tile(a.out, base, nrows, nrows, mine, 0, r0, r1, r2, r3);
 }
 
 // rk45_simple_current (rkf45.py:672-724) over ncol columns, one lane each.
@@ -3074,11 +3069,6 @@ struct rwrt_ctx {
   int quad_per_wave = 16;      // latency mode: rays per wave (rwrt_ctx_set_latency_density)
   int64_t* trace = nullptr;    // rwrt_ctx_set_trace (diagnostic)
   int64_t trace_cap = 0;
-  int32_t slice_rows = 0;      // rwrt_ctx_set_slicing (0: off)
-  // sliced queue scratch: [0, 16) qlen (int64), then progress int32[slice_cap],
-  // then the hand-off records uint64[slice_cap][16] (128-B aligned)
-  char* slices = nullptr;
-  size_t slice_cap = 0;
   bool used = false;
   std::mutex mu;
 };
@@ -3110,27 +3100,10 @@ rwrt_status ctx_flags(rwrt_ctx* c, int64_t nray) {
     c->cap = 0;
   }
   const size_t cap = ((size_t)nray + 4095) & ~(size_t)4095;
-  if (hipMalloc(reinterpret_cast<void**>(&c->flags), cap) != hipSuccess)
+  // (+128 B: the queue extent, queue_extent_kernel)
+  if (hipMalloc(reinterpret_cast<void**>(&c->flags), cap + 128) != hipSuccess)
     return fail(RWRT_ERR_HIP, "frozen-ray flag allocation failed%s");
   c->cap = cap;
-  return RWRT_OK;
-}
-
-size_t slice_progress_bytes(size_t cap) { return (cap * sizeof(int32_t) + 127) & ~(size_t)127; }
-
-// Sliced-queue scratch for n queue positions (released like the flags).
-rwrt_status ctx_slices(rwrt_ctx* c, int64_t n) {
-  if ((size_t)n <= c->slice_cap && c->slices) return RWRT_OK;
-  if (c->slices) {
-    if ((c->used && hipEventSynchronize(c->done) != hipSuccess) || hipFree(c->slices) != hipSuccess)
-      return check_launch("releasing the context's slice scratch");
-    c->slices = nullptr;
-    c->slice_cap = 0;
-  }
-  const size_t cap = ((size_t)n + 4095) & ~(size_t)4095;
-  if (hipMalloc(reinterpret_cast<void**>(&c->slices), 128 + slice_progress_bytes(cap) + cap * 128) != hipSuccess)
-    return fail(RWRT_ERR_HIP, "slice scratch allocation failed%s");
-  c->slice_cap = cap;
   return RWRT_OK;
 }
 
@@ -3178,8 +3151,14 @@ template <class BG>
 rwrt_status launch_run(rwrt_ctx* ctx, const BG& B, int64_t nray, const rwrt_params* p,
                        const double* d_tbound, int32_t it_begin, int32_t it_end,
                        const int64_t* d_order, int64_t n_heavy, double* d_state, int64_t* d_count,
-                       int32_t* d_nanrow, double* d_out, int32_t* d_work, void* stream) {
+                       int32_t* d_nanrow, double* d_out, int32_t* d_work, void* stream,
+                       int32_t* d_rowpos = nullptr, double* d_prev = nullptr, int32_t out_rows = 0,
+                       double budget_us = 0.0, double grace_us = -1.0) {
   if (rwrt_status s = ctx_check(ctx)) return s;
+  if (!(budget_us >= 0.0 && budget_us < 1e12) || !(grace_us < 1e12))
+    return fail(RWRT_ERR_ARG, "budget_us / grace_us out of range%s");
+  if (out_rows == 0) out_rows = it_end - it_begin;
+  if (out_rows < it_end - it_begin) return fail(RWRT_ERR_ARG, "out_rows < it_end - it_begin%s");
   if (!p) return fail(RWRT_ERR_ARG, "params is NULL%s");
   if (nray < 0 || nray > 0x7fffffffLL) return fail(RWRT_ERR_ARG, "nray out of range%s");
   if (it_begin < 1 || it_end > p->nt || it_begin >= it_end)
@@ -3221,9 +3200,19 @@ rwrt_status launch_run(rwrt_ctx* ctx, const BG& B, int64_t nray, const rwrt_para
   // waits for the fill, so the call stays one stream-ordered operation
   if (rwrt_status s = ctx_flags(ctx, nray)) return s;
   a.frozen = ctx->flags;
+  a.rowpos = d_rowpos;
+  a.prev = d_prev;
+  a.out_nrows = out_rows;
+  a.budget = (uint64_t)(budget_us * 100.0);   // s_memrealtime: 100 MHz
+  a.grace = grace_us >= 0.0 ? (uint64_t)(grace_us * 100.0) : ~0ull;
+  unsigned long long* qlen = reinterpret_cast<unsigned long long*>(ctx->flags + ctx->cap);
+  a.qlen = reinterpret_cast<const int64_t*>(qlen);
   if (rwrt_status s = ctx_begin(ctx, st, [&] {
         hipLaunchKernelGGL(frozen_flag_kernel, dim3(grid_for(nray, 256)), dim3(256), 0, st, d_state, nray,
                            ctx->flags);
+        if (hipMemsetAsync(qlen, 0, sizeof(*qlen), st) == hipSuccess && nray > n_heavy)
+          hipLaunchKernelGGL(queue_extent_kernel, dim3(grid_for(nray - n_heavy, 256)), dim3(256), 0, st, d_order,
+                             nray, n_heavy, ctx->flags, d_rowpos, it_end, qlen);
       }))
     return s;
   // latency mode in the run kernel's first team_blocks blocks (quad_rays):
@@ -3232,22 +3221,6 @@ rwrt_status launch_run(rwrt_ctx* ctx, const BG& B, int64_t nray, const rwrt_para
   // wait for a CU on its XCD until the persistent grid drains)
   a.heavy_blocks = (int32_t)team_blocks;
   a.quad_per_wave = quad_per_wave;
-  // row slicing: (queue position, slice) items over the positions live at the start
-  const int64_t rows = it_end - it_begin;
-  const int64_t nslices = ctx->slice_rows > 0 ? (rows + ctx->slice_rows - 1) / ctx->slice_rows : 1;
-  if (nslices > 1 && nray > n_heavy && nslices * (nray - n_heavy) < 0x7fffffffLL - (1LL << 24)) {
-    if (rwrt_status s = ctx_slices(ctx, nray - n_heavy)) return s;
-    a.slice_rows = ctx->slice_rows;
-    a.nslices = (int32_t)nslices;
-    a.qlen = reinterpret_cast<const int64_t*>(ctx->slices);
-    a.progress = reinterpret_cast<int32_t*>(ctx->slices + 128);
-    a.handoff = reinterpret_cast<uint64_t*>(ctx->slices + 128 + slice_progress_bytes(ctx->slice_cap));
-    if (hipMemsetAsync(ctx->slices, 0, 128 + (size_t)(nray - n_heavy) * sizeof(int32_t), st) != hipSuccess)
-      return check_launch("hipMemsetAsync(slice progress)");
-    hipLaunchKernelGGL(queue_extent_kernel, dim3(grid_for(nray - n_heavy, 256)), dim3(256), 0, st, d_order, nray,
-                       n_heavy, ctx->flags, reinterpret_cast<unsigned long long*>(ctx->slices));
-    if (rwrt_status s = check_launch("queue_extent_kernel")) return s;
-  }
   if constexpr (std::is_same<BG, StaticBG>::value) {
     a.trace = ctx->trace;
     a.trace_cap = ctx->trace ? ctx->trace_cap : 0;
@@ -3453,14 +3426,6 @@ rwrt_status rwrt_ctx_set_latency_density(rwrt_ctx* c, int32_t rays_per_wave) {
   return RWRT_OK;
 }
 
-rwrt_status rwrt_ctx_set_slicing(rwrt_ctx* c, int32_t slice_rows) {
-  if (!c) return fail(RWRT_ERR_ARG, "rwrt_ctx is NULL%s");
-  if (slice_rows < 0) return fail(RWRT_ERR_ARG, "slice_rows must be >= 0%s");
-  std::lock_guard<std::mutex> lock(c->mu);
-  c->slice_rows = slice_rows;
-  return RWRT_OK;
-}
-
 rwrt_status rwrt_ctx_set_trace(rwrt_ctx* c, int64_t* d_trace, int64_t capacity) {
   if (!c) return fail(RWRT_ERR_ARG, "rwrt_ctx is NULL%s");
   if (capacity < 0 || (capacity > 0 && !d_trace) || capacity > 0x7fffffffLL)
@@ -3480,7 +3445,6 @@ rwrt_status rwrt_ctx_destroy(rwrt_ctx* c) {
     // the last call's kernels may still read the flags / run on the side stream
     if (c->used && hipEventSynchronize(c->done) != hipSuccess) s = check_launch("rwrt_ctx_destroy");
     if (c->flags) (void)hipFree(c->flags);
-    if (c->slices) (void)hipFree(c->slices);
     if (c->side) (void)hipStreamDestroy(c->side);
     if (c->flagged) (void)hipEventDestroy(c->flagged);
     if (c->filled) (void)hipEventDestroy(c->filled);
@@ -3575,6 +3539,20 @@ rwrt_status rwrt_rk45_run(rwrt_ctx* ctx, const rwrt_grid* g, const double* d_pac
   if (rwrt_status s = make_field(g, d_packed, F)) return s;
   return launch_run(ctx, StaticBG{F}, nray, p, d_tbound, it_begin, it_end, d_order, n_heavy, d_state,
                     d_count, d_nanrow, d_out, d_work, stream);
+}
+
+rwrt_status rwrt_rk45_run_budget(rwrt_ctx* ctx, const rwrt_grid* g, const double* d_packed,
+                                 int64_t nray, const rwrt_params* p, const double* d_tbound,
+                                 int32_t it_begin, int32_t it_end, const int64_t* d_order,
+                                 int64_t n_heavy, double* d_state, int64_t* d_count, int32_t* d_nanrow,
+                                 int32_t* d_rowpos, double* d_prev, double* d_out, int32_t out_rows,
+                                 int32_t* d_work, double budget_us, double grace_us, void* stream) {
+  Field F;
+  if (rwrt_status s = make_field(g, d_packed, F)) return s;
+  if (nray > 0 && (!d_rowpos || !d_prev)) return fail(RWRT_ERR_ARG, "d_rowpos / d_prev is NULL%s");
+  if (out_rows < it_end - it_begin) return fail(RWRT_ERR_ARG, "out_rows < it_end - it_begin%s");
+  return launch_run(ctx, StaticBG{F}, nray, p, d_tbound, it_begin, it_end, d_order, n_heavy, d_state,
+                    d_count, d_nanrow, d_out, d_work, stream, d_rowpos, d_prev, out_rows, budget_us, grace_us);
 }
 
 rwrt_status rwrt_rk45_init_tv(const rwrt_grid* g, const rwrt_background* b, int64_t nray,

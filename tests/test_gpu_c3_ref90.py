@@ -29,7 +29,7 @@ from make_devmath import row_hashes  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 
-def run_c3_90d(kind, team="auto", slice_rows=0):
+def run_c3_90d(kind, team="auto", phases=None):
     """Rows [7, 1081, n] and (nacc, nrej) of the fixture's sample, from a
     full-set 90-day run with the bench's schedule."""
     import torch
@@ -40,7 +40,6 @@ def run_c3_90d(kind, team="auto", slice_rows=0):
     nt = int(g["nt"])
     bs, _ = make_bs(kind)
     eng = RayEngine.from_bs(bs)
-    eng.ctx.set_slicing(slice_rows)
     src, zcs = c3_sources(eng)
     rows0 = torch.cat([eng.initial_rows_dev(src, zc)[0].reshape(7, -1) for zc in zcs], dim=1)
     assert rows0.shape[1] == int(g["nslot"])
@@ -59,7 +58,7 @@ def run_c3_90d(kind, team="auto", slice_rows=0):
         hist[:, i0:i1, p[m].cpu().numpy()] = np.transpose(got, (2, 1, 0))
 
     r = run_sharded(eng, rows0[:5].contiguous(), nt, 7200.0, rank=0, world=1, probe=6, lead=[24, 160],
-                    chunk=nt - 1, sink=sink, ttotal=(nt - 1) * 7200.0, team=team)
+                    chunk=nt - 1, sink=sink, ttotal=(nt - 1) * 7200.0, team=team, phases=phases)
     counts = torch.empty((rows0.shape[1], 2), dtype=torch.int64, device=eng.device)
     counts[r.idx] = r.counts
     counts = counts[idx].cpu().numpy()
@@ -95,12 +94,15 @@ def test_c3_90d_sample_latency_mode_bitwise():
     check(g, hist, counts)
 
 
-@pytest.mark.parametrize("kind", ["zonal", "nonzonal"])
-def test_c3_90d_sample_sliced_queue_bitwise(kind):
-    """The sliced work queue (rwrt_ctx_set_slicing, 7-row slices: a ray's 890-row
-    launch is 128 work items, its solver state handed between lanes, CUs and
-    XCDs 127 times) gives the same bits as one item per ray."""
-    g, hist, counts = run_c3_90d(kind, slice_rows=7)
+@pytest.mark.parametrize("kind,team,targets", [("zonal", 0, []), ("nonzonal", 0, []),
+                                               ("zonal", 128, [20, 60, 120, 240, 480, 720, 900])])
+def test_c3_90d_sample_phases_bitwise(kind, team, targets):
+    """Scheduling phases (rwrt_rk45_run_budget: every phase ends 1 ms after its
+    queue ran empty, its stragglers stopped after an accepted step -- inside a
+    row -- and resumed from there by whichever lane takes them next phase, the
+    queue re-ordered by estimated work left; with the 128 heaviest rays of
+    every phase in latency mode) give the same bits."""
+    g, hist, counts = run_c3_90d(kind, team=team, phases=targets)
     check(g, hist, counts)
 
 
