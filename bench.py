@@ -311,10 +311,6 @@ def main():
     ap.add_argument("--split", default="auto", choices=["auto", "off"],
                     help="split the long launch once more when the leading launches' per-ray work "
                          "predicts the next poorly (RayEngine.SPLIT_RHO)")
-    ap.add_argument("--phases", default=None,
-                    help="C3: run the rows after the probe in scheduling phases (RayEngine.advance_budgeted) "
-                         "with these comma-separated row targets ('default': RayEngine.PHASE_TARGETS; "
-                         "'off': row launches)")
     ap.add_argument("--team", default="auto",
                     help="rays per launch in latency mode (quad_rays: four lanes of a wave per ray); "
                          "an integer or 'auto' (RayEngine.team_size)")
@@ -421,10 +417,6 @@ def main():
     lead = [int(x) for x in str(args.first_chunk).split(",") if x]
     team = args.team if args.team == "auto" else int(args.team)
     split = None if args.split == "off" else args.split
-    phases = (None if args.phases in (None, "off")
-              else [] if args.phases == "default"
-              else {"budgets": [1e3 * float(x) for x in args.phases[2:].split(",")]} if args.phases.startswith("t:")
-              else [int(x) for x in str(args.phases).split(",") if x])
     gather_dev = torch.device("cpu") if backend == "gloo" else dev
     n_live_max = n_live
     if weak and dist:
@@ -455,12 +447,12 @@ def main():
         if weak:
             r = run_sharded(eng, y, nt, 7200.0, rank=0, world=1, probe=args.probe, lead=lead,
                             chunk=chunk, out=out, events=events, ttotal=(nt - 1) * 7200.0,
-                            order_policy=args.order, team=team, split=split, phases=phases)
+                            order_policy=args.order, team=team, split=split)
             gather_endpoints(r)
             return r
         return run_sharded(eng, y, nt, 7200.0, group=group, probe=args.probe, lead=lead,
                            chunk=chunk, out=out, events=events, ttotal=(nt - 1) * 7200.0,
-                           order_policy=args.order, team=team, split=split, phases=phases)
+                           order_policy=args.order, team=team, split=split)
 
     for _ in range(args.warmup):
         one_step()
@@ -502,8 +494,7 @@ def main():
                     + (" (BASELINE configs[2])" if world == 1 else
                        (" per GPU, the seed grid shifted by rank x 2/N deg of longitude (BASELINE configs[3], "
                         "weak scaling)" if weak else " (BASELINE configs[3]: C4, one set split)")))
-        schedule = ([args.probe] + [b - a for a, b in r.res.bounds] if phases is None
-                    else [args.probe, r.res.bounds[-1][1] - r.res.bounds[0][0]])
+        schedule = [args.probe] + [b - a for a, b in r.res.bounds]
         if weak:
             par = (f"{world} rank(s), one GPU each (backend {backend or 'none'}): each integrates its own "
                    f"C3 seed grid (2.40 M slots), no exchange during integration; inside the timed step "
@@ -522,9 +513,6 @@ def main():
             "config": {"workload": workload,
                        "ray_slots": nslot * (world if weak else 1), "live_rays_rank0": n_live,
                        "rows": nt, "rows_per_launch": chunk, "launch_rows": schedule,
-                       "phases": (None if phases is None else
-                                  {"row_targets": [b for a, b in r.res.bounds],
-                                   "grace_us": eng.GRACE_US, "spec": args.phases}),
                        "rank0_rays": n_mine,
                        "latency_mode": ("per launch, the heaviest rays whose move to quad_rays (four lanes of a "
                                         "wave per ray) minimises the predicted makespan by >= 10 %"

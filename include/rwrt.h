@@ -203,29 +203,6 @@ rwrt_status rwrt_rk45_run(rwrt_ctx* ctx, const rwrt_grid* g, const double* d_pac
                           int32_t* d_nanrow, double* d_out, int32_t* d_work,
                           void* stream);
 
-/* rwrt_rk45_run in scheduling phases, for ray sets whose rays' work is uneven
- * and hard to predict (RayEngine.advance_budgeted: a few calls per row range,
- * the queue re-ordered in between).  d_out holds rows [it_begin, it_begin +
- * out_rows) of every ray (out_rows >= it_end - it_begin); each ray continues
- * from its own position d_rowpos[ray] (it_begin <= d_rowpos <= it_end; set
- * it to it_begin, and d_prev[2][nray] to the rays' lon, lat, before the
- * first call of a row range) toward row it_end, and the call ends early:
- * budget_us > 0 microseconds after its kernel started, or grace_us >= 0
- * microseconds after its work queue ran empty (< 0: not).  A ray then stops
- * after its next accepted step -- inside a row or at its end, where the
- * reference's loop state is complete (wr.py:808-887: y, f, t, h_abs and the
- * row's reference position for the jump mask, d_prev) -- and d_rowpos
- * records the row it is in.  Rows, counters and states do not depend on the
- * budgets, the orders or the row targets used. */
-rwrt_status rwrt_rk45_run_budget(rwrt_ctx* ctx, const rwrt_grid* g, const double* d_packed,
-                                 int64_t nray, const rwrt_params* p,
-                                 const double* d_tbound, int32_t it_begin,
-                                 int32_t it_end, const int64_t* d_order,
-                                 int64_t n_heavy, double* d_state, int64_t* d_count,
-                                 int32_t* d_nanrow, int32_t* d_rowpos, double* d_prev,
-                                 double* d_out, int32_t out_rows, int32_t* d_work,
-                                 double budget_us, double grace_us, void* stream);
-
 /* Fixed-step RK4 ray loop, the reference's default integrator:
  * WR.core_ray_run_numpy (wr.py:702-765) with rk4_step_numpy (wr.py:583-622)
  * and core_rk4_step (wr.py:89-95), for rows it_begin <= i < it_end, dt =

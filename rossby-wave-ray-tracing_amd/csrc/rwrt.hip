@@ -1835,38 +1835,6 @@ struct RunArgs {
   int32_t quad_per_wave = 16;  // latency mode: rays per wave (1..16; fewer = less divergence per ray)
   int64_t* trace = nullptr;    // diagnostic ray trace (rwrt_ctx_set_trace), positions < trace_cap
   int64_t trace_cap = 0;
-  // budgeted calls (rwrt_rk45_run_budget): each ray continues from rowpos[ray]
-  // and, once `budget` ticks of s_memrealtime (100 MHz) have passed since its
-  // wave started, stops at its next output row and records it there
-  int32_t* rowpos = nullptr;   // NULL: every ray runs rows [it_begin, it_end)
-  double* prev = nullptr;      // [2][nray] lon, lat of the row before rowpos (the jump mask's reference)
-  uint64_t budget = 0;         // 0: no deadline
-  uint64_t grace = ~0ull;      // stop this long after the queue has drained (~0: never)
-  const int64_t* qlen = nullptr;  // queue positions after n_heavy that can hold work (queue_extent_kernel)
-  int32_t out_nrows = 0;       // rows per ray of d_out (which starts at row it_begin)
-};
-
-// Wave-uniform end of a budgeted call: `budget` ticks after the wave started,
-// or `grace` ticks after the wave first saw the work queue drained -- the
-// real-time counter (and the queue head) read every 32nd iteration of the ray
-// loop (~0.4 ms of a wave)
-struct Deadline {
-  uint64_t at = ~0ull;
-  uint32_t tick = 0;
-  bool passed = false, armed = false;
-  __device__ __forceinline__ Deadline(uint64_t budget, uint64_t grace) {
-    armed = budget || grace != ~0ull;
-    if (budget) at = __builtin_amdgcn_s_memrealtime() + budget;
-  }
-  template <class A>
-  __device__ __forceinline__ void poll(const A& a, int64_t qend) {
-    if (!armed || passed || (++tick & 31u) != 0) return;
-    const uint64_t now = __builtin_amdgcn_s_memrealtime();
-    if (a.grace != ~0ull && at - now > a.grace &&
-        a.n_heavy + __hip_atomic_load(&a.queue[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= qend)
-      at = now + a.grace;   // the queue has drained: the stragglers stop soon
-    passed = now >= at;
-  }
 };
 
 // rwrt_ctx_set_trace: where (HW_ID, XCC) and when a traced ray ran
@@ -2174,6 +2142,7 @@ __device__ __forceinline__ void quad_rays(const RunArgs<StaticBG>& a, char* cach
   R.odd = (R.role & 1) != 0;
   R.high = (R.role & 2) != 0;
   KQuad K{Kq + threadIdx.x};
+  const int64_t nrows = a.it_end - a.it_begin;
   // order position of this quad's ray: the heaviest rays one per wave first
   // (position p -> wave p % waves, quad p / waves), a.quad_per_wave quads per wave
   const int qi = (threadIdx.x & 63) >> 2;
@@ -2196,17 +2165,12 @@ __device__ __forceinline__ void quad_rays(const RunArgs<StaticBG>& a, char* cach
   const int64_t att0 = nacc + nrej;
   if (kTrace && w < a.trace_cap && R.role == 0) trace_start(a.trace, w);
   int32_t nanrow = a.nanrow[ray];
-  int32_t it = a.rowpos ? a.rowpos[ray] : a.it_begin;
-  if (it >= a.it_end) return;   // (budgeted calls: done in an earlier one)
-  double prev_lon = a.prev ? a.prev[ray] : y[0], prev_lat = a.prev ? a.prev[a.nray + ray] : y[1];
-  double cos_prev = k_cos(prev_lat);
+  int32_t it = a.it_begin;
+  double prev_lon = y[0], prev_lat = y[1], cos_prev = k_cos(prev_lat);
   aux[2] = kNaN;
   bool in_step = false, rejected = false;
   const bool writer = R.role == 0;
-  const int64_t qend = a.n_heavy + (a.qlen ? *a.qlen : a.nray - a.n_heavy);
-  Deadline dl(a.budget, a.grace);
   for (;;) {
-    dl.poll(a, qend);
     const double tb = a.tbound[it];
     // ---- Lane::iterate (rkf45.py:222-253, 375-514)
     int st = 0;   // 0 step, 1 reached, 2 frozen
@@ -2249,10 +2213,7 @@ __device__ __forceinline__ void quad_rays(const RunArgs<StaticBG>& a, char* cach
       rejected = rejected || !acc;
       nacc += acc ? 1 : 0;
       nrej += acc ? 0 : 1;
-      if (!(acc && t - tb >= 0.0)) {
-        if (dl.passed && acc) break;   // (budgeted: stop inside row it after an accepted step)
-        continue;
-      }
+      if (!(acc && t - tb >= 0.0)) continue;
       st = 1;
     }
     // ---- interval it reached: rk45_run_kernel's post-processing (wr.py:835-885)
@@ -2280,7 +2241,7 @@ __device__ __forceinline__ void quad_rays(const RunArgs<StaticBG>& a, char* cach
       const double2 r0 = make_double2(y[0], y[1]), r1 = make_double2(y[2], y[3]);
       const double2 r2 = make_double2(y[4], ug), r3 = make_double2(vg, (double)nacc);
       for (int kr = it; kr < last; ++kr) {
-        double2* o = reinterpret_cast<double2*>(a.out + ((size_t)ray * a.out_nrows + (kr - a.it_begin)) * RWRT_NOUT);
+        double2* o = reinterpret_cast<double2*>(a.out + ((size_t)ray * nrows + (kr - a.it_begin)) * RWRT_NOUT);
         o[0] = r0;
         o[1] = r1;
         o[2] = r2;
@@ -2293,14 +2254,9 @@ __device__ __forceinline__ void quad_rays(const RunArgs<StaticBG>& a, char* cach
     cos_prev = cos_c;
     it = last;
     if (st == 2) t = a.tbound[a.it_end - 1];
-    if (it == a.it_end || dl.passed) break;
+    if (it == a.it_end) break;
   }
   if (writer) {
-    if (a.rowpos) {
-      a.rowpos[ray] = it;
-      a.prev[ray] = prev_lon;
-      a.prev[a.nray + ray] = prev_lat;
-    }
 #pragma unroll
     for (int v = 0; v < 5; ++v) {
       a.state[v * a.nray + ray] = y[v];
@@ -2324,29 +2280,6 @@ __device__ __forceinline__ void quad_rays(const RunArgs<StaticBG>& a, char* cach
 // latency mode (quad_rays in the grid's first blocks, order[0, n_heavy)); the
 // queue is the rest.
 using KStore = KShared<5>;
-
-// A ray leaves its lane: its solver state (and, in budgeted calls, the row it
-// is in and that row's reference position) back to the per-ray arrays
-template <class A>
-__device__ __forceinline__ void retire_ray(const A& a, int64_t ray, int32_t it, const double* y, const double* f,
-                                           double t, double habs, int64_t nacc, int64_t nrej, int32_t nanrow,
-                                           double prev_lon, double prev_lat) {
-#pragma unroll
-  for (int v = 0; v < 5; ++v) {
-    a.state[v * a.nray + ray] = y[v];
-    a.state[(5 + v) * a.nray + ray] = f[v];
-  }
-  a.state[10 * a.nray + ray] = t;
-  a.state[11 * a.nray + ray] = habs;
-  a.count[2 * ray] = nacc;
-  a.count[2 * ray + 1] = nrej;
-  a.nanrow[ray] = nanrow;
-  if (a.rowpos) {
-    a.rowpos[ray] = it;
-    a.prev[ray] = prev_lon;
-    a.prev[a.nray + ray] = prev_lat;
-  }
-}
 // kTrace: the diagnostic instantiation (rwrt_ctx_set_trace) -- the product
 // kernel carries none of the trace hooks
 template <class BG, bool kTrace = false>
@@ -2365,6 +2298,7 @@ __global__ void __launch_bounds__(256, 1) rk45_run_kernel(RunArgs<BG> a) {
     }
   }
   const RayProblem P{LaneBG<BG>::make(a.B, smem + kKBytes)};
+  const int64_t nrows = a.it_end - a.it_begin;
   Lane<RayProblem, KStore> L;
   L.K.p = reinterpret_cast<double*>(smem) + threadIdx.x;
   L.K.stride = 256;
@@ -2376,25 +2310,16 @@ __global__ void __launch_bounds__(256, 1) rk45_run_kernel(RunArgs<BG> a) {
     // fill takes the issue cycles the ray loop leaves idle
     __builtin_amdgcn_s_setprio(1);
   }
-  const int64_t qend = a.n_heavy + (a.qlen ? *a.qlen : a.nray - a.n_heavy);
-  Deadline dl(a.budget, a.grace);
   for (;;) {
-    dl.poll(a, qend);
     if (ray < 0) {
-      if (dl.passed) break;
       const int64_t w = a.n_heavy + atomicAdd(&a.queue[1], 1);
-      if (w >= qend) break;
+      if (w >= a.nray) break;
       ray = a.order ? a.order[w] : w;
       if (kTrace) {
         wpos = (int32_t)w;
         if (w < a.trace_cap) trace_start(a.trace, w);
       }
       if (a.frozen && a.frozen[ray]) {   // its rows come from frozen_fill_kernel
-        ray = -1;
-        continue;
-      }
-      it = a.rowpos ? a.rowpos[ray] : a.it_begin;
-      if (it >= a.it_end) {   // (budgeted calls: done in an earlier one)
         ray = -1;
         continue;
       }
@@ -2411,27 +2336,15 @@ __global__ void __launch_bounds__(256, 1) rk45_run_kernel(RunArgs<BG> a) {
       nacc = a.count[2 * ray];
       nrej = a.count[2 * ray + 1];
       nanrow = a.nanrow[ray];
+      it = a.it_begin;
       prev_lon = L.y[0];   // == rlon[it-1], rlat[it-1] (wr.py:844, 877-885)
       prev_lat = L.y[1];
-      if (a.prev) {        // (budgeted calls: the ray may have stopped inside row it)
-        prev_lon = a.prev[ray];
-        prev_lat = a.prev[a.nray + ray];
-      }
       cos_prev = k_cos(prev_lat);
       L.aux[2] = kNaN;     // no evaluation at y yet
     }
     const double tb = a.tbound[it];
     const int st = L.iterate(P, tb, a.min_step, a.rtol, a.atol, nacc, nrej);
-    if (st == Lane<RayProblem, KStore>::kStep) {
-      // (budgeted calls past their end: stop inside row it after an accepted
-      // step -- the loop state is then y, f, t, h_abs and the row's reference
-      // position, as after any accepted step)
-      if (!(dl.passed && !L.in_step)) continue;
-      asm volatile("");
-      retire_ray(a, ray, it, L.y, L.f, L.t, L.habs, nacc, nrej, nanrow, prev_lon, prev_lat);
-      ray = -1;
-      continue;
-    }
+    if (st == Lane<RayProblem, KStore>::kStep) continue;
 
     // ---- interval it reached: post-processing (wr.py:835-885) ----
     // The last accepted step's K6 evaluation was at this y: its cos(lat), ug
@@ -2467,7 +2380,7 @@ __global__ void __launch_bounds__(256, 1) rk45_run_kernel(RunArgs<BG> a) {
     // equals this one: write them all and release the lane.
     const int last = (st == Lane<RayProblem, KStore>::kFrozen) ? a.it_end : it + 1;
     if (!0) {   // (timing-only diagnostic build: no row stores)
-      double2* o = reinterpret_cast<double2*>(a.out + ((size_t)ray * a.out_nrows + (it - a.it_begin)) * RWRT_NOUT);
+      double2* o = reinterpret_cast<double2*>(a.out + ((size_t)ray * nrows + (it - a.it_begin)) * RWRT_NOUT);
       store_row16<0>(o + 0, r0);
       store_row16<0>(o + 1, r1);
       store_row16<0>(o + 2, r2);
@@ -2476,7 +2389,7 @@ __global__ void __launch_bounds__(256, 1) rk45_run_kernel(RunArgs<BG> a) {
     if (!0 && last > it + 1) {
       asm volatile("");   // frozen: the remaining rows of the chunk (rare branch)
       for (int k = it + 1; k < last; ++k) {
-        double2* o = reinterpret_cast<double2*>(a.out + ((size_t)ray * a.out_nrows + (k - a.it_begin)) * RWRT_NOUT);
+        double2* o = reinterpret_cast<double2*>(a.out + ((size_t)ray * nrows + (k - a.it_begin)) * RWRT_NOUT);
         o[0] = r0;
         o[1] = r1;
         o[2] = r2;
@@ -2489,10 +2402,19 @@ __global__ void __launch_bounds__(256, 1) rk45_run_kernel(RunArgs<BG> a) {
     cos_prev = cos_c;
     it = last;
     if (st == Lane<RayProblem, KStore>::kFrozen) L.t = a.tbound[a.it_end - 1];
-    if (it == a.it_end || dl.passed) {   // the call's end, or its deadline at this row
+    if (it == a.it_end) {
+#pragma unroll
+      for (int v = 0; v < 5; ++v) {
+        a.state[v * a.nray + ray] = y[v];
+        a.state[(5 + v) * a.nray + ray] = L.f[v];
+      }
+      a.state[10 * a.nray + ray] = L.t;
+      a.state[11 * a.nray + ray] = L.habs;
       if (kTrace && wpos < a.trace_cap)
         trace_ray(a.trace, wpos, ray, nacc + nrej - a.count[2 * ray] - a.count[2 * ray + 1], false);
-      retire_ray(a, ray, it, y, L.f, L.t, L.habs, nacc, nrej, nanrow, prev_lon, prev_lat);
+      a.count[2 * ray] = nacc;
+      a.count[2 * ray + 1] = nrej;
+      a.nanrow[ray] = nanrow;
       ray = -1;
     }
   }
@@ -2521,26 +2443,6 @@ __global__ void frozen_flag_kernel(const double* __restrict__ state, int64_t nra
   }
 }
 
-// The queue's end: one past the last position (after the latency-mode
-// entries) whose ray has work in the call -- live at its start and, in a
-// budgeted call, not yet at it_end -- so that lanes do not walk the frozen and
-// finished rays the engine's orders put last (70 % of C3's slots).
-__global__ void queue_extent_kernel(const int64_t* __restrict__ order, int64_t nray, int64_t n_heavy,
-                                    const uint8_t* __restrict__ frozen, const int32_t* __restrict__ rowpos,
-                                    int32_t it_end, unsigned long long* __restrict__ qlen) {
-  unsigned long long m = 0;
-  for (int64_t p = n_heavy + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < nray;
-       p += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t r = order ? order[p] : p;
-    if (!frozen[r] && (!rowpos || rowpos[r] < it_end)) m = (unsigned long long)(p - n_heavy + 1);
-  }
-  for (int o = 32; o > 0; o >>= 1) {   // the wave's maximum, then one atomic per wave
-    const unsigned long long x = __shfl_xor(m, o);
-    m = x > m ? x : m;
-  }
-  if ((threadIdx.x & 63) == 0 && m) atomicMax(qlen, m);
-}
-
 // At most 128 VGPRs: a fill wave must fit beside the run kernel's wave in a
 // SIMD's register file (256 VGPRs + its AGPRs of 512), and its LDS (the 3.5
 // KB sin/cos table, one wave per block) beside the run kernel's 155 KB, or
@@ -2551,16 +2453,14 @@ constexpr int kFillThreads = 64;
 // ray's rows are); thread t stores quarter t & 3 of the 64-B row, read from
 // the ray's lane by cross-lane reads -- no LDS, so that a fill wave fits
 // beside rk45_run_kernel's 155 KB block on every CU.
-__device__ __forceinline__ void write_frozen_tile(double* out, int64_t base, int64_t nrows, int64_t last,
-                                                  bool mine, int32_t first, double2 r0, double2 r1, double2 r2,
-                                                  double2 r3) {
+__device__ __forceinline__ void write_frozen_tile(double* out, int64_t base, int64_t nrows, bool mine,
+                                                  double2 r0, double2 r1, double2 r2, double2 r3) {
   unsigned long long lanes = __ballot(mine);
-  const int64_t nq = last * 4;   // rows [first, last) of each ray's nrows
+  const int64_t nq = nrows * 4;
   const int qt = threadIdx.x & 3;
   while (lanes) {
     const int j = __builtin_ctzll(lanes);
     lanes &= lanes - 1;
-    const int64_t qfirst = 4 * (int64_t)__shfl(first, j);   // the ray's first row of the call (rowpos)
     double2* o = reinterpret_cast<double2*>(out + (size_t)(base + j) * nrows * RWRT_NOUT);
     // (every lane reads lane j's quarters 0..3 in turn and keeps its own)
     const double2 q0 = make_double2(__shfl(r0.x, j), __shfl(r0.y, j));
@@ -2568,11 +2468,11 @@ __device__ __forceinline__ void write_frozen_tile(double* out, int64_t base, int
     const double2 q2 = make_double2(__shfl(r2.x, j), __shfl(r2.y, j));
     const double2 q3 = make_double2(__shfl(r3.x, j), __shfl(r3.y, j));
     const double2 v = qt == 0 ? q0 : qt == 1 ? q1 : qt == 2 ? q2 : q3;
-    for (int64_t q = qfirst + threadIdx.x; q < nq; q += kFillThreads) store_row16<1>(o + q, v);
+    for (int64_t q = threadIdx.x; q < nq; q += kFillThreads) store_row16<1>(o + q, v);
     // pace the stores (~0.9 us per full 64 rows written; none for shorter
     // chunks): a full-rate fill floods the memory queues the run kernel's
     // lookups wait in
-    for (int64_t z = 64; z <= last - qfirst / 4; z += 64) __builtin_amdgcn_s_sleep(32);
+    for (int64_t z = 64; z <= nrows; z += 64) __builtin_amdgcn_s_sleep(32);
   }
 }
 
@@ -2580,12 +2480,10 @@ template <class BG>
 __global__ void __launch_bounds__(kFillThreads) __attribute__((amdgpu_num_vgpr(128)))
 frozen_fill_kernel(RunArgs<BG> a) {
   nm_stage<NM_SINCOS>();
+  const int64_t nrows = a.it_end - a.it_begin;
   const int64_t base = blockIdx.x * (int64_t)kFillThreads;
   const int64_t ray = base + threadIdx.x;
-  // (budgeted calls: a ray frozen in an earlier call of the row range wrote
-  // its rows to it_end there; rowpos = it_end)
-  const int32_t it = (ray < a.nray && a.rowpos) ? a.rowpos[ray] : a.it_begin;
-  const bool mine = ray < a.nray && a.frozen[ray] && it < a.it_end;
+  const bool mine = ray < a.nray && a.frozen[ray];
   double2 r0 = make_double2(0.0, 0.0), r1 = r0, r2 = r0, r3 = r0;
   if (mine) {
     // rk45_run_kernel's fetch + kFrozen iteration + post-processing, verbatim
@@ -2594,6 +2492,7 @@ frozen_fill_kernel(RunArgs<BG> a) {
     for (int v = 0; v < 5; ++v) y[v] = a.state[v * a.nray + ray];
     const int64_t nacc = a.count[2 * ray];
     int32_t nanrow = a.nanrow[ray];
+    const int32_t it = a.it_begin;
     const double prev_lon = y[0], prev_lat = y[1];
     const double cos_prev = k_cos(prev_lat);
     const double tb = a.tbound[it];
@@ -2619,9 +2518,8 @@ frozen_fill_kernel(RunArgs<BG> a) {
     for (int v = 0; v < 5; ++v) a.state[v * a.nray + ray] = y[v];
     a.state[10 * a.nray + ray] = a.tbound[a.it_end - 1];
     a.nanrow[ray] = nanrow;
-    if (a.rowpos) a.rowpos[ray] = a.it_end;
   }
-  write_frozen_tile(a.out, base, a.out_nrows, a.it_end - a.it_begin, mine, it - a.it_begin, r0, r1, r2, r3);
+  write_frozen_tile(a.out, base, nrows, mine, r0, r1, r2, r3);
 }
 
 
@@ -2841,7 +2739,7 @@ rk4_fill_kernel(Rk4Args a) {
     a.count[2 * ray] = nstep;
     a.nanrow[ray] = nanrow;
   }
-  write_frozen_tile(a.out, base, nrows, nrows, mine, 0, r0, r1, r2, r3);
+  write_frozen_tile(a.out, base, nrows, mine, r0, r1, r2, r3);
 }
 
 // rk45_simple_current (rkf45.py:672-724) over ncol columns, one lane each.
@@ -3100,8 +2998,7 @@ rwrt_status ctx_flags(rwrt_ctx* c, int64_t nray) {
     c->cap = 0;
   }
   const size_t cap = ((size_t)nray + 4095) & ~(size_t)4095;
-  // (+128 B: the queue extent, queue_extent_kernel)
-  if (hipMalloc(reinterpret_cast<void**>(&c->flags), cap + 128) != hipSuccess)
+  if (hipMalloc(reinterpret_cast<void**>(&c->flags), cap) != hipSuccess)
     return fail(RWRT_ERR_HIP, "frozen-ray flag allocation failed%s");
   c->cap = cap;
   return RWRT_OK;
@@ -3151,14 +3048,8 @@ template <class BG>
 rwrt_status launch_run(rwrt_ctx* ctx, const BG& B, int64_t nray, const rwrt_params* p,
                        const double* d_tbound, int32_t it_begin, int32_t it_end,
                        const int64_t* d_order, int64_t n_heavy, double* d_state, int64_t* d_count,
-                       int32_t* d_nanrow, double* d_out, int32_t* d_work, void* stream,
-                       int32_t* d_rowpos = nullptr, double* d_prev = nullptr, int32_t out_rows = 0,
-                       double budget_us = 0.0, double grace_us = -1.0) {
+                       int32_t* d_nanrow, double* d_out, int32_t* d_work, void* stream) {
   if (rwrt_status s = ctx_check(ctx)) return s;
-  if (!(budget_us >= 0.0 && budget_us < 1e12) || !(grace_us < 1e12))
-    return fail(RWRT_ERR_ARG, "budget_us / grace_us out of range%s");
-  if (out_rows == 0) out_rows = it_end - it_begin;
-  if (out_rows < it_end - it_begin) return fail(RWRT_ERR_ARG, "out_rows < it_end - it_begin%s");
   if (!p) return fail(RWRT_ERR_ARG, "params is NULL%s");
   if (nray < 0 || nray > 0x7fffffffLL) return fail(RWRT_ERR_ARG, "nray out of range%s");
   if (it_begin < 1 || it_end > p->nt || it_begin >= it_end)
@@ -3200,19 +3091,9 @@ rwrt_status launch_run(rwrt_ctx* ctx, const BG& B, int64_t nray, const rwrt_para
   // waits for the fill, so the call stays one stream-ordered operation
   if (rwrt_status s = ctx_flags(ctx, nray)) return s;
   a.frozen = ctx->flags;
-  a.rowpos = d_rowpos;
-  a.prev = d_prev;
-  a.out_nrows = out_rows;
-  a.budget = (uint64_t)(budget_us * 100.0);   // s_memrealtime: 100 MHz
-  a.grace = grace_us >= 0.0 ? (uint64_t)(grace_us * 100.0) : ~0ull;
-  unsigned long long* qlen = reinterpret_cast<unsigned long long*>(ctx->flags + ctx->cap);
-  a.qlen = reinterpret_cast<const int64_t*>(qlen);
   if (rwrt_status s = ctx_begin(ctx, st, [&] {
         hipLaunchKernelGGL(frozen_flag_kernel, dim3(grid_for(nray, 256)), dim3(256), 0, st, d_state, nray,
                            ctx->flags);
-        if (hipMemsetAsync(qlen, 0, sizeof(*qlen), st) == hipSuccess && nray > n_heavy)
-          hipLaunchKernelGGL(queue_extent_kernel, dim3(grid_for(nray - n_heavy, 256)), dim3(256), 0, st, d_order,
-                             nray, n_heavy, ctx->flags, d_rowpos, it_end, qlen);
       }))
     return s;
   // latency mode in the run kernel's first team_blocks blocks (quad_rays):
@@ -3539,20 +3420,6 @@ rwrt_status rwrt_rk45_run(rwrt_ctx* ctx, const rwrt_grid* g, const double* d_pac
   if (rwrt_status s = make_field(g, d_packed, F)) return s;
   return launch_run(ctx, StaticBG{F}, nray, p, d_tbound, it_begin, it_end, d_order, n_heavy, d_state,
                     d_count, d_nanrow, d_out, d_work, stream);
-}
-
-rwrt_status rwrt_rk45_run_budget(rwrt_ctx* ctx, const rwrt_grid* g, const double* d_packed,
-                                 int64_t nray, const rwrt_params* p, const double* d_tbound,
-                                 int32_t it_begin, int32_t it_end, const int64_t* d_order,
-                                 int64_t n_heavy, double* d_state, int64_t* d_count, int32_t* d_nanrow,
-                                 int32_t* d_rowpos, double* d_prev, double* d_out, int32_t out_rows,
-                                 int32_t* d_work, double budget_us, double grace_us, void* stream) {
-  Field F;
-  if (rwrt_status s = make_field(g, d_packed, F)) return s;
-  if (nray > 0 && (!d_rowpos || !d_prev)) return fail(RWRT_ERR_ARG, "d_rowpos / d_prev is NULL%s");
-  if (out_rows < it_end - it_begin) return fail(RWRT_ERR_ARG, "out_rows < it_end - it_begin%s");
-  return launch_run(ctx, StaticBG{F}, nray, p, d_tbound, it_begin, it_end, d_order, n_heavy, d_state,
-                    d_count, d_nanrow, d_out, d_work, stream, d_rowpos, d_prev, out_rows, budget_us, grace_us);
 }
 
 rwrt_status rwrt_rk45_init_tv(const rwrt_grid* g, const rwrt_background* b, int64_t nray,

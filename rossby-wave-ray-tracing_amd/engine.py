@@ -373,26 +373,6 @@ class RayEngine:
             H.dptr(st["count"]), H.dptr(st["nanrow"]), H.dptr(out, F64), H.dptr(self.work),
             self._stream()))
 
-    def run_budget(self, st, p, tbound, it_begin, it_end, out, rowpos, prev, budget_us=0.0, grace_us=-1.0,
-                   order=None, n_heavy=0, rays_per_wave=16):
-        """``run`` in a scheduling phase (rwrt_rk45_run_budget): each ray from
-        its own position ``rowpos`` (int32 [nray]; ``prev`` [2, nray] the
-        lon, lat of the row before it) toward row ``it_end``; ``out`` holds
-        rows ``[it_begin, it_begin + out.shape[1])``.  The call ends
-        ``budget_us`` after it started (> 0) or ``grace_us`` after its queue
-        ran empty (>= 0); every ray then stops after its next accepted step and
-        ``rowpos`` / ``prev`` record where.  Static background only."""
-        if self.bg is not None:
-            raise NotImplementedError("budgeted calls run on the static basic state")
-        if n_heavy:
-            self.ctx.set_latency_density(rays_per_wave)
-        H.check(H.load().rwrt_rk45_run_budget(
-            self.ctx.handle, self.grid, H.dptr(self.packed), st["nray"], ctypes_ref(p), H.dptr(tbound, F64),
-            int(it_begin), int(it_end), H.dptr(order, torch.int64), int(n_heavy), H.dptr(st["state"]),
-            H.dptr(st["count"]), H.dptr(st["nanrow"]), H.dptr(rowpos, torch.int32, "rowpos"),
-            H.dptr(prev, F64, "prev"), H.dptr(out, F64), int(out.shape[1]), H.dptr(self.work),
-            float(budget_us), float(grace_us), self._stream()))
-
     def integrate_rk4(self, y0, nt, tstep, cut_off=0.1, chunk=None, sink=None, out=None,
                       cut_rad=None, events=None, group=None):
         """The fixed-step RK4 ray loop (wr.py:702-765) for ``y0[5, nray]``.
@@ -442,8 +422,7 @@ class RayEngine:
 
     def integrate(self, y0, nt, tstep, rtol=1e-6, atol=1e-6, msf=1e-3, cut_off=0.1,
                   ttotal=None, chunk=None, sink=None, out=None, cut_rad=None, events=None,
-                  group=None, order_policy="priority", first_chunk=None, team=0, stop_row=None,
-                  phases=None):
+                  group=None, order_policy="priority", first_chunk=None, team=0, stop_row=None):
         """The whole ray loop for ``y0[5, nray]``; rows 1..nt-1 go to ``sink``.
 
         ``sink(i0, i1, rows)`` receives each time chunk as a device tensor
@@ -455,8 +434,7 @@ class RayEngine:
         integrated in latency mode per launch (rk45_team_kernel: each ray's
         RHS over the four SIMDs of a CU) -- an int (the heaviest rays by the
         previous launch's work, or the first live ones before any) or "auto"
-        (``team_size``).  ``phases``: rows 1..nt-1 in scheduling phases with
-        these row targets (``advance_budgeted``; static background).  ``events`` (a list) collects a pair of timing
+        (``team_size``).  ``events`` (a list) collects a pair of timing
         events around every ray-loop launch.  With a process ``group`` (rays
         sharded over ranks, shard.py) the two global outcomes -- solver
         failure and the all-NaN early exit -- are decided over every rank, so a
@@ -479,10 +457,6 @@ class RayEngine:
             # rkf45.py:423-425: at the first step every live column has a NaN
             # h_abs -> status -1 -> wr.py:886-887 breaks before storing row 1.
             return RunResult(cnt[:, 0], cnt[:, 1], st["nanrow"], True, 1, n_live)
-        if phases is not None:
-            # (the phases' row targets, or () for the default ones)
-            return self.advance_budgeted(st, p, tb, 1, targets=phases or None, sink=sink, out=out,
-                                         events=events, group=group, n_live=n_live, team=team)
         return self.advance(st, p, tb, 1, chunk=chunk, sink=sink, out=out, events=events,
                             group=group, order_policy=order_policy, first_chunk=first_chunk,
                             n_live=n_live, n_live_local=n_live_local, team=team, stop_row=stop_row)
@@ -600,85 +574,6 @@ class RayEngine:
         res = RunResult(cnt[:, 0], cnt[:, 1], st["nanrow"], False, brk, n_live)
         res.bounds = bounds
         res.state, res.next_row = st, end
-        res.params = run_params(p, tb)
-        return res
-
-    # Scheduling phases (advance_budgeted).  A launch per row range is list
-    # scheduling whose makespan is its heaviest ray's chain of attempts, and
-    # every launch boundary makes that ray wait for the rest of the launch
-    # (tools/tail_trace.py: both C3 backgrounds' last launches are bound by
-    # ONE ray's attempts).  Instead, each phase advances every ray toward a
-    # row target and ends GRACE_US after its work queue ran empty: the rays
-    # still short of the target then stop after their next accepted step --
-    # inside a row if need be -- and lead the next phase, whose queue is
-    # ordered by each ray's estimated work left to its target (its latest
-    # attempts per row x rows to go, longest first).  No lane waits for a
-    # straggler; the stragglers never wait for a launch's end.
-    PHASE_TARGETS = (31, 191, 491)   # rows; the last phase runs to nt
-    GRACE_US = 1000.0
-
-    def advance_budgeted(self, st, p, tb, start, targets=None, grace_us=None, sink=None, out=None, events=None,
-                         group=None, n_live=None, prev_work=None, team=0, budgets=None):
-        """Rows ``[start, nt)`` of the ray loop in scheduling phases (above),
-        one per row target (then nt).  ``prev_work`` (attempts at the start of
-        the launch that ran rows ``[1, start)``, e.g. the probe) gives each
-        ray's first attempts-per-row estimate; ``team``: rays per phase in
-        latency mode, the first of the order.  Rows reach ``sink(start, nt,
-        rows)`` once, after the last phase.  Same results as ``advance``."""
-        nt = int(p.nt)
-        nray = st["nray"]
-        cnt = st["count"]
-        if n_live is None:
-            n_live = int((~torch.isnan(st["state"][:5].sum(0))).sum().item())
-        if budgets is not None:
-            # time-budgeted phases toward nt (each ray runs on until a phase's
-            # budget is spent), then one to the end
-            targets = [nt] * (len(budgets) + 1)
-            budgets = [float(b) for b in budgets] + [0.0]
-        else:
-            targets = [int(t) for t in (self.PHASE_TARGETS if targets is None else targets) if start < int(t) < nt]
-            targets.append(nt)
-            budgets = [0.0] * len(targets)
-        grace = self.GRACE_US if grace_us is None else float(grace_us)
-        rows = nt - start
-        bufs = _row_buffers(out, nray, rows, self.device)
-        view = bufs[0].view(-1)[: nray * rows * H.NOUT].view(nray, rows, H.NOUT)
-        rowpos = torch.full((nray,), int(start), dtype=torch.int32, device=self.device)
-        prev = st["state"][:2].clone()
-        att = cnt.sum(1).to(F64)
-        base = torch.zeros_like(att) if prev_work is None else prev_work.to(F64)
-        rate = (att - base) / max(int(start) - 1, 1)          # attempts per row so far
-        self.phase_log = []
-        for k, target in enumerate(targets):
-            last = k == len(targets) - 1
-            frozen = torch.isnan(st["state"][:5].sum(0))
-            togo = (target - rowpos).clamp(min=0).to(F64)
-            key = torch.where(frozen | (togo <= 0), torch.full_like(togo, -1.0), rate * togo.clamp(min=1.0))
-            order = torch.sort(key, descending=True, stable=True).indices.to(torch.int64).contiguous()
-            n_heavy, qpw = (self.team_size(team, st, key, order, target - start) if team else (0, 16))
-            att0, row0 = cnt.sum(1).to(F64), rowpos.clone()
-            if events is not None:
-                e0, e1, es = self._event_pair()
-            self.run_budget(st, p, tb, start, target, view, rowpos, prev, budgets[k],
-                            -1.0 if (last or budgets[k] > 0) else grace, order, n_heavy, qpw)
-            if events is not None:
-                e1.record(es)
-                events.append((e0, e1))
-            adv = (rowpos - row0).to(F64)
-            da = cnt.sum(1).to(F64) - att0
-            # a ray that advanced: its attempts per row in this phase; one that
-            # ran without finishing a row: at least those attempts per row
-            rate = torch.where(adv > 0, da / adv.clamp(min=1.0), torch.maximum(rate, da))
-            self.phase_log.append((int(target), int(n_heavy)))
-        if sink is not None:
-            sink(start, nt, view)
-        mx = int(st["nanrow"].max().item()) if nray else 0
-        if group is not None:
-            from shard import reduce_max
-            mx = reduce_max(mx, group)
-        res = RunResult(cnt[:, 0], cnt[:, 1], st["nanrow"], False, mx if mx < nt else None, n_live)
-        res.bounds = [(start, t) for t in targets]
-        res.state, res.next_row = st, nt
         res.params = run_params(p, tb)
         return res
 

@@ -207,7 +207,7 @@ class ShardedRun:
 
 def run_sharded(eng, y0, nt, tstep=7200.0, group=None, rank=None, world=None, probe=6,
                 lead=(24, 96), chunk=None, out=None, sink=None, events=None, gather=True,
-                ttotal=None, order_policy="priority", team=0, split=None, phases=None):
+                ttotal=None, order_policy="priority", team=0, split=None):
     """One ray set ``y0[5, nray]`` (identical on every rank) integrated across
     the ranks of ``group``.
 
@@ -216,9 +216,7 @@ def run_sharded(eng, y0, nt, tstep=7200.0, group=None, rank=None, world=None, pr
     the attempts each ray needed there decide the split (``cost_partition``).
     Each rank then integrates only its own rays to ``nt`` and ``gather`` sends
     their last row and step counters to rank 0 (RCCL ``gather`` on device
-    tensors).  ``phases`` (a list of row targets; empty: the defaults) runs
-    the rows after the probe in scheduling phases instead of launches
-    (``RayEngine.advance_budgeted``).  ``sink(i0, i1, rows, idx)`` receives this rank's rows.
+    tensors).  ``sink(i0, i1, rows, idx)`` receives this rank's rows.
     ``team`` is ``RayEngine.advance``'s latency-mode size per launch, ``split``
     its adaptive split of the long launch.
     ``rank``/``world`` without a group emulate one rank of a larger job on
@@ -258,29 +256,10 @@ def run_sharded(eng, y0, nt, tstep=7200.0, group=None, rank=None, world=None, pr
 
     keep(1, 1 + npr, prow[idx])
     n_live_local = int((~frozen[idx]).sum().item())
-    if phases is not None and isinstance(phases, dict):
-        # (experiment) the lead launches, then time-budgeted phases to the end
-        start = 1 + npr
-        pw = torch.zeros_like(cost[idx])
-        if lead:
-            stop = 1 + npr + sum(lead)
-            r0 = eng.advance(local, p, tb, start, chunk=chunk, sink=keep, out=out, events=events, group=group,
-                             order_policy=order_policy, first_chunk=list(lead), n_live=int(summary[0]),
-                             n_live_local=n_live_local, prev_work=pw, team=0, stop_row=stop)
-            start = stop
-        res = eng.advance_budgeted(local, p, tb, start, sink=keep, out=out, events=events, group=group,
-                                   n_live=int(summary[0]), prev_work=torch.zeros_like(cost[idx]), team=team,
-                                   budgets=phases["budgets"])
-    elif phases is not None:
-        # one row range after the probe, in budgeted calls (RayEngine.advance_budgeted)
-        res = eng.advance_budgeted(local, p, tb, 1 + npr, targets=phases or None, sink=keep, out=out,
-                                   events=events, group=group, n_live=int(summary[0]),
-                                   prev_work=torch.zeros_like(cost[idx]), team=team)
-    else:
-        res = eng.advance(local, p, tb, 1 + npr, chunk=chunk, sink=keep, out=out, events=events,
-                          group=group, order_policy=order_policy, first_chunk=list(lead),
-                          n_live=int(summary[0]), n_live_local=n_live_local,
-                          prev_work=torch.zeros_like(cost[idx]), team=team, split=split)
+    res = eng.advance(local, p, tb, 1 + npr, chunk=chunk, sink=keep, out=out, events=events,
+                      group=group, order_policy=order_policy, first_chunk=list(lead),
+                      n_live=int(summary[0]), n_live_local=n_live_local,
+                      prev_work=torch.zeros_like(cost[idx]), team=team, split=split)
     steps_local = int(local["count"][:, 0].sum().item())
     ends = cnts = None
     if gather:

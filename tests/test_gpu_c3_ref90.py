@@ -29,7 +29,7 @@ from make_devmath import row_hashes  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 
-def run_c3_90d(kind, team="auto", phases=None):
+def run_c3_90d(kind, team="auto"):
     """Rows [7, 1081, n] and (nacc, nrej) of the fixture's sample, from a
     full-set 90-day run with the bench's schedule."""
     import torch
@@ -58,7 +58,7 @@ def run_c3_90d(kind, team="auto", phases=None):
         hist[:, i0:i1, p[m].cpu().numpy()] = np.transpose(got, (2, 1, 0))
 
     r = run_sharded(eng, rows0[:5].contiguous(), nt, 7200.0, rank=0, world=1, probe=6, lead=[24, 160],
-                    chunk=nt - 1, sink=sink, ttotal=(nt - 1) * 7200.0, team=team, phases=phases)
+                    chunk=nt - 1, sink=sink, ttotal=(nt - 1) * 7200.0, team=team)
     counts = torch.empty((rows0.shape[1], 2), dtype=torch.int64, device=eng.device)
     counts[r.idx] = r.counts
     counts = counts[idx].cpu().numpy()
@@ -91,18 +91,6 @@ def test_c3_90d_sample_bitwise_with_reference_arithmetic(kind):
 
 def test_c3_90d_sample_latency_mode_bitwise():
     g, hist, counts = run_c3_90d("zonal", team=1024)
-    check(g, hist, counts)
-
-
-@pytest.mark.parametrize("kind,team,targets", [("zonal", 0, []), ("nonzonal", 0, []),
-                                               ("zonal", 128, [20, 60, 120, 240, 480, 720, 900])])
-def test_c3_90d_sample_phases_bitwise(kind, team, targets):
-    """Scheduling phases (rwrt_rk45_run_budget: every phase ends 1 ms after its
-    queue ran empty, its stragglers stopped after an accepted step -- inside a
-    row -- and resumed from there by whichever lane takes them next phase, the
-    queue re-ordered by estimated work left; with the 128 heaviest rays of
-    every phase in latency mode) give the same bits."""
-    g, hist, counts = run_c3_90d(kind, team=team, phases=targets)
     check(g, hist, counts)
 
 

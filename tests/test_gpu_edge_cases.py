@@ -163,44 +163,3 @@ def test_rk4_chunked_runs_equal_one_launch():
     with np.errstate(all="ignore"):
         href, _ = O.ray_run_rk4(O.Background(**bg), rows7[:5].copy(), nt, 7200.0, row0=rows7)
     assert _same(np.transpose(h2[:, 1:, :7], (2, 1, 0)), href[:, 1:])
-
-
-@pytest.mark.parametrize("n,targets,team", [(300, [3, 5, 6, 9, 11, 14, 17, 20, 22], 0),
-                                             (2048, [4, 8, 12, 16, 20], 64), (129, [], 0)])
-def test_phases_bitwise(n, targets, team):
-    """rwrt_rk45_run_budget in scheduling phases: each ray continues from its
-    own row toward the phase's row target, a phase ends 1 ms after its queue
-    ran empty and its stragglers stop after an accepted step inside a row
-    (rays that freeze in one phase and are skipped by the next, dead slots,
-    the latency mode's rays stopped and resumed too) -- bitwise the oracle's."""
-    eng, bg = _engine("nonzonal")
-    rows = golden("init_C2_nonzonal.npz")["rows"][:5].reshape(5, -1)
-    rng = np.random.default_rng(n)
-    pick = rng.choice(rows.shape[1], min(n, rows.shape[1]), replace=False)
-    y0 = np.ascontiguousarray(rows[:, pick])
-    out = {}
-    res = eng.integrate(torch.as_tensor(y0), NT, 7200.0, ttotal=(NT - 1) * 7200.0, team=team, phases=targets,
-                        sink=lambda a, b, o: out.__setitem__((a, b), o.cpu().numpy().copy()))
-    assert list(out) == [(1, NT)]
-    hist = np.full((y0.shape[1], NT, 8), np.nan)
-    hist[:, 1:] = out[(1, NT)]
-    _check(hist, res, _oracle(bg, y0, NT))
-    assert res.ray_steps > 0
-
-
-def test_phase_stops_inside_rows_bitwise():
-    """grace 0: every phase ends as soon as its queue is empty, so lanes still
-    inside a row stop there after their next accepted step (many mid-row stops
-    per ray) -- bitwise the oracle's."""
-    eng, bg = _engine("zonal")
-    eng.GRACE_US = 0.0
-    rows = golden("init_C2_zonal.npz")["rows"][:5].reshape(5, -1)
-    live = np.flatnonzero(~np.isnan(rows.sum(0)))
-    y0 = np.ascontiguousarray(rows[:, live[:4096]])
-    out = {}
-    res = eng.integrate(torch.as_tensor(y0), NT, 7200.0, ttotal=(NT - 1) * 7200.0,
-                        phases=list(range(2, NT, 2)),
-                        sink=lambda a, b, o: out.__setitem__((a, b), o.cpu().numpy().copy()))
-    hist = np.full((y0.shape[1], NT, 8), np.nan)
-    hist[:, 1:] = out[(1, NT)]
-    _check(hist, res, _oracle(bg, y0, NT))

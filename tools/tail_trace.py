@@ -1,6 +1,6 @@
 """When every ray of a C3 launch runs (rwrt_ctx_set_trace on all queue positions).
 
-    python tools/tail_trace.py [--bg nonzonal zonal] [--phases default|31,191,491] [--team N] [--out DIR]
+    python tools/tail_trace.py [--bg nonzonal zonal] [--team N] [--out DIR]
 
 Runs the bench's C3 schedule on one GPU (probe, the 24- and 160-row launches,
 the adaptive split, the rest) and traces every queue position of the LAST
@@ -9,8 +9,8 @@ launch times, how many rays are still running at each tenth of the last
 launch, and the rays that end last (their queue position, attempts, and the
 attempts the order predicted them by); writes DIR/tail_<bg>.npz (position,
 start, end in microseconds from the launch's first start, attempts, predicted
-attempts).  ``--phases`` runs the rows after the probe in scheduling phases
-(RayEngine.advance_budgeted): the trace is the last phase's.
+attempts).  (The scheduling-phase runs of round 3 used the reverted
+rwrt_rk45_run_budget: profiles/r3/phases/.)
 """
 import argparse
 import json
@@ -26,7 +26,6 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "rossby-wave-ray-tracing_amd")]
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--bg", nargs="+", default=["nonzonal", "zonal"])
-    ap.add_argument("--phases", default=None)
     ap.add_argument("--team", type=int, default=0)
     ap.add_argument("--split", default="auto")
     ap.add_argument("--out", default=None)
@@ -45,8 +44,6 @@ def main():
         trace = torch.zeros((nray, 10), dtype=torch.int64, device=eng.device)
         launches = []
         saved = torch.zeros_like(trace)
-        phases = (None if a.phases is None else [] if a.phases == "default"
-                  else [int(x) for x in a.phases.split(",")])
 
         def sink(i0, i1, rows, idx):
             # stream-ordered after launch [i0, i1): keep its trace, clear for the next
@@ -56,8 +53,7 @@ def main():
         ev = []
         eng.ctx.set_trace(trace)
         r = run_sharded(eng, y0, nt, 7200.0, rank=0, world=1, probe=6, lead=[24, 160], chunk=nt - 1,
-                        sink=sink, events=ev, ttotal=(nt - 1) * 7200.0, team=a.team, split=a.split,
-                        phases=phases)
+                        sink=sink, events=ev, ttotal=(nt - 1) * 7200.0, team=a.team, split=a.split)
         torch.cuda.synchronize()
         eng.ctx.set_trace(None)
         trace = saved
@@ -74,7 +70,7 @@ def main():
         T = t1.max()
         prof = [int(((t0 <= f * T) & (t1 > f * T)).sum()) for f in np.linspace(0, 1, 11)[:-1]]
         last = np.argsort(-t1)[:20]
-        info = {"bg": kind, "phases": a.phases, "team": a.team, "launches": launches, "launch_s": launch_s,
+        info = {"bg": kind, "team": a.team, "launches": launches, "launch_s": launch_s,
                 "step_s": sum(launch_s), "traced": int(ok.sum()), "last_launch_us": float(T),
                 "rays_running_at_tenths": prof,
                 "median_end_us": float(np.median(t1)), "p99_end_us": float(np.percentile(t1, 99)),
@@ -84,7 +80,7 @@ def main():
         print(json.dumps(info), flush=True)
         if a.out:
             os.makedirs(a.out, exist_ok=True)
-            np.savez_compressed(os.path.join(a.out, f"tail_{kind}_p{(a.phases or 'off').replace(',', '-')}_t{a.team}.npz"), pos=pos.astype(np.int32),
+            np.savez_compressed(os.path.join(a.out, f"tail_{kind}_t{a.team}.npz"), pos=pos.astype(np.int32),
                                 t0=t0.astype(np.float32), t1=t1.astype(np.float32), att=att.astype(np.int32),
                                 launch_s=np.array(launch_s))
         del eng, r, y0, trace
