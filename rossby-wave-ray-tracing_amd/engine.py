@@ -302,7 +302,8 @@ class RayEngine:
     # heavy ray in a full run (tools/team_latency.py --density, 90 d: 16 / 64
     # / 256 heaviest rays 0.20 / 0.21 / 0.21 s at 16 per wave, 0.51 / 0.55 /
     # 0.56 s at 1 per wave, 256 rays 0.27 s at 4 per wave), so only 16
-    QUAD_DENSITIES = (16,)
+    # (RWRT_QUAD_DENSITIES=4,16 lets the rule consider others: A/B only)
+    QUAD_DENSITIES = tuple(int(x) for x in os.environ.get("RWRT_QUAD_DENSITIES", "16").split(","))
 
     def team_capacity(self):
         """Rays the latency mode takes at most (64 per CU, half the CUs)."""
