@@ -32,6 +32,15 @@
 //   NM_ADD_RD(a,b)   addition rounded toward -infinity
 //   NM_FALLBACK_SIN/COS/TAN/POW  library routines outside the domain above
 // Compile with -ffp-contract=off: every fused operation here is explicit.
+//
+// Provenance and licences of what is restated: the algorithms and constants
+// of glibc's IBM Accurate Mathematical Library (sysdeps/ieee754/dbl-64/
+// s_sin.c, sincostab; GNU LGPL-2.1-or-later) and of Intel's SVML kernels
+// shipped inside NumPy (numpy/_core/src/umath/svml; BSD-3-Clause).  No source
+// file of either is copied: the operation sequences were read from the
+// machine code of the two shared objects of the reference's host and the
+// constants extracted from them (tools/gen_np_math.py); the reference
+// repository itself contains none of this code.
 #pragma once
 
 #include "np_math_tables.h"

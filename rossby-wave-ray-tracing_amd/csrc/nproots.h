@@ -20,6 +20,13 @@
 // -ffp-contract=off).  Verified bit-for-bit against numpy's eigvals on the
 // reference host (tests/test_nproots.py).  Compiled for the device (init
 // kernel) and, for that test only, for the host.
+//
+// Provenance and licences of the restated algorithms: LAPACK 3.12 (ZGEBAL,
+// ZLAHQR, ZLARFG, DLADIV, DLAPY3; modified BSD), OpenBLAS 0.3.29 (dznrm2,
+// zscal kernels; BSD-3-Clause), NumPy's npymath complex division
+// (BSD-3-Clause), glibc 2.35 hypot / csqrt (LGPL-2.1-or-later).  Written from
+// the published algorithms and checked against their results; no source
+// file of those projects is copied.
 #pragma once
 #include <cstdint>
 #include <cstring>

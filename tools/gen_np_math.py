@@ -135,6 +135,7 @@ def main():
     rA, rN, sha = rcp14_knots()
 
     lines = ["// GENERATED by tools/gen_np_math.py -- do not edit.",
+             "// (constants of glibc libm, LGPL-2.1-or-later, and of NumPy's SVML kernels, BSD-3-Clause)",
              "// Constants and tables of the reference NumPy's transcendentals (see np_math.h):",
              f"//   glibc: {LIBM} (__sin_fma / __cos_fma, sincostab at 0xaeb80)",
              f"//   numpy: {os.path.basename(npso)} (numpy {np.__version__}): __svml_tan8_ha, __svml_pow8_ha",
