@@ -164,7 +164,7 @@ def find_profile(name, path, workload, schedule):
     return fallback
 
 
-def roofline(steps_per_launch, avg_launch_s, workload, schedule, bytes_per_step, args):
+def roofline(steps_per_launch, avg_launch_s, workload, schedule, bytes_per_step, args, bound="valu_issue"):
     """The ray-loop kernel against the bound it hits: VALU issue at one wave per
     SIMD.  VALU wave-instructions per launch and the in-kernel clock come from
     the PMC profile of this build and schedule (tools/pmc_valu.py), the launch
@@ -201,6 +201,14 @@ def roofline(steps_per_launch, avg_launch_s, workload, schedule, bytes_per_step,
                           "note": ("SURVEY.md 8(d): 6 RHS x 4 corners x 11 fields x 8 B per accepted step; "
                                    "most lookups are served by the per-lane LDS cell cache and L2, so this "
                                    "is a yardstick, not HBM traffic, and can exceed the HBM peak")}
+    if bound == "hbm":
+        # C5: the 0.25-degree levels are gathered from HBM / MALL (one level per
+        # lane cached in LDS): the memory roofline leads, VALU issue beside it
+        valu_part = {k: out[k] for k in ("achieved", "peak", "unit", "frac", "note") if k in out}
+        out.update(bound="hbm", unit="GB/s", peak=HBM_PEAK / 1e9, achieved=out["hbm"]["achieved_GBps"],
+                   frac=out["hbm"]["frac"], valu_issue=valu_part,
+                   note=("PMC line traffic (FETCH_SIZE x2 + WRITE_SIZE, calibrated on this access pattern: "
+                         "DESIGN.md 4, C5 traffic) per launch over the launch's HIP-event time"))
     return out
 
 
@@ -746,7 +754,7 @@ def main_c5(args, dist, group, rank, world, dev, share=1):
             "queue_order": args.order,
             "library_sha256": library_sha(),
             "init": "GPU rwrt_ray_initial inside every timed step",
-            "roofline": roofline(per_launch_steps, avg_launch_s, workload, schedule, bps, args)}))
+            "roofline": roofline(per_launch_steps, avg_launch_s, workload, schedule, bps, args, bound="hbm")}))
     if dist:
         dist.barrier()
         dist.destroy_process_group()
