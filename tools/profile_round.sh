@@ -17,3 +17,6 @@ python3 tools/pmc_traffic.py $out/fetch $out/write $out/trace.log $sum/traffic.j
 python3 tools/pmc_valu.py $out/valu $out/trace.log $sum/valu.json
 cp $out/valu/run_counter_collection.csv $sum/valu_counters.csv
 grep -h '^{' $out/trace.log > $sum/bench_under_rocprof.json || true
+# keep the summaries only (the raw per-dispatch CSVs of a long run exceed
+# gpurun's 64 MiB merge-back limit)
+rm -rf $out/trace $out/fetch $out/write $out/valu
