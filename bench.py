@@ -319,9 +319,11 @@ def main():
     ap.add_argument("--split", default="auto", choices=["auto", "off"],
                     help="split the long launch once more when the leading launches' per-ray work "
                          "predicts the next poorly (RayEngine.SPLIT_RHO)")
-    ap.add_argument("--team", default="auto",
+    ap.add_argument("--team", default=None,
                     help="rays per launch in latency mode (quad_rays: four lanes of a wave per ray); "
-                         "an integer or 'auto' (RayEngine.team_size)")
+                         "an integer, one per launch after the probe (e.g. 64,256,64; the last "
+                         "repeats) or 'auto' (RayEngine.team_size).  Default: 64,256,64 for a whole C3 "
+                         "set per GPU, auto for a split one")
     ap.add_argument("--lib", default=None, help="alternative librwrt build (A/B timing)")
     ap.add_argument("--traffic", default=None, help="traffic.json (tools/pmc_traffic.py)")
     ap.add_argument("--valu-profile", default=None, help="valu.json (tools/pmc_valu.py)")
@@ -340,6 +342,13 @@ def main():
         # (heavy-ray-bound) and C5: 24 + 96
         whole = world == 1 or args.scaling == "weak"
         args.first_chunk = "24,160" if (args.config == "C3" and whole) else "24,96"
+    if args.team is None:
+        # a whole C3 set per GPU: the 160-row launch is bound by its heaviest
+        # rays' chains -- 256 of them in latency mode there, 64 in the other
+        # launches (profiles/r3/sched/pass_u_team_per_launch.txt: +0.9 % over
+        # none, two repetitions each); a split set: the auto rule
+        whole = world == 1 or args.scaling == "weak"
+        args.team = "64,256,64" if (args.config == "C3" and whole) else "auto"
     if args.lib:
         os.environ["RWRT_LIB"] = os.path.abspath(args.lib)
 
@@ -423,7 +432,8 @@ def main():
     chunk = args.chunk or max(1, min(nt - 1, int(0.8 * free) // (n_local * 64)))
     out = torch.empty((n_local, min(chunk, nt - 1), 8), dtype=torch.float64, device=dev)
     lead = [int(x) for x in str(args.first_chunk).split(",") if x]
-    team = args.team if args.team == "auto" else int(args.team)
+    team = (args.team if args.team == "auto" else
+            [x if x == "auto" else int(x) for x in args.team.split(",")] if "," in args.team else int(args.team))
     split = None if args.split == "off" else args.split
     gather_dev = torch.device("cpu") if backend == "gloo" else dev
     n_live_max = n_live
@@ -525,7 +535,8 @@ def main():
                        "latency_mode": ("per launch, the heaviest rays whose move to quad_rays (four lanes of a "
                                         "wave per ray) minimises the predicted makespan by >= 10 %"
                                         if args.team == "auto"
-                                        else f"{args.team} rays per launch in latency mode (quad_rays)"),
+                                        else f"{args.team} heaviest rays per launch after the probe in "
+                                             f"latency mode (quad_rays, four lanes of a wave per ray)"),
                        "parallelism": par},
             "ray_steps_per_step": tot_steps / args.steps,
             "ray_steps_per_step_rank0": steps_done / args.steps,

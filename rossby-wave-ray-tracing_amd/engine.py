@@ -551,7 +551,9 @@ class RayEngine:
                 # the previous launch's attempts per ray, or ("total") all of them so far
                 work = cnt.sum(1) - (0 if order_policy == "total" else prev_work)
                 order = self.cost_cell_order(st, work) if order_policy == "cell" else self.cost_order(st, work)
-            n_heavy, qpw = self.team_size(team, st, work, order, i1 - i0) if team else (0, 16)
+            # (a list: one latency-mode size per launch, the last repeated)
+            tk = team[min(k, len(team) - 1)] if isinstance(team, list) else team
+            n_heavy, qpw = self.team_size(tk, st, work, order, i1 - i0) if tk else (0, 16)
             if os.environ.get("RWRT_DEBUG_TEAM"):
                 print(f"launch rows [{i0}, {i1}): n_heavy {n_heavy} at {qpw} per wave", flush=True)
             prev_work = cnt.sum(1)

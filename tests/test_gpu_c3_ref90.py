@@ -89,8 +89,11 @@ def test_c3_90d_sample_bitwise_with_reference_arithmetic(kind):
     assert int((~np.isnan(hist[0, -1])).sum()) > hist.shape[2] // 2
 
 
-def test_c3_90d_sample_latency_mode_bitwise():
-    g, hist, counts = run_c3_90d("zonal", team=1024)
+@pytest.mark.parametrize("team", [1024, [64, 256, 64]])
+def test_c3_90d_sample_latency_mode_bitwise(team):
+    """The heaviest rays of every launch in latency mode (quad_rays): 1 024 per
+    launch, and the bench's per-launch default (64 / 256 / 64)."""
+    g, hist, counts = run_c3_90d("zonal", team=team)
     check(g, hist, counts)
 
 
