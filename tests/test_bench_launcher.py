@@ -60,3 +60,25 @@ def test_failing_rank_ends_the_run():
     # non-zero instead of hanging
     p, lines = _bench(["--gpus", "2", "--dry-run"], {"RWRT_DIST_BACKEND": "no_such_backend"})
     assert p.returncode != 0 and not lines
+
+
+def test_roofline_hbm_bound_for_c5(tmp_path):
+    """C5 lines lead with the HBM roofline (PMC line traffic per launch over
+    the launch time) and keep the VALU-issue figures beside it."""
+    import json
+    import bench
+    prof = {"workload": "w", "launch_rows": [6, 24], "library_sha256": "x", "valu_insts_per_launch": 1e9,
+            "clock_hz": 2.4e9, "simds": 1024, "cycles_per_valu": 4}
+    traf = dict(prof, traffic_bytes_per_launch=4e11)
+    (tmp_path / "valu.json").write_text(json.dumps(prof))
+    (tmp_path / "traffic.json").write_text(json.dumps(traf))
+
+    class A:
+        valu_profile = str(tmp_path / "valu.json")
+        traffic = str(tmp_path / "traffic.json")
+    r = bench.roofline(1e6, 0.1, "w", [6, 24], 4224, A, bound="hbm")
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s"
+    assert abs(r["achieved"] - 4000.0) < 1e-6 and abs(r["frac"] - 0.5) < 1e-9
+    assert abs(r["valu_issue"]["frac"] - 1e9 / 0.1 / (1024 * 2.4e9 / 4)) < 1e-9
+    v = bench.roofline(1e6, 0.1, "w", [6, 24], 2112, A)
+    assert v["bound"] == "valu_issue" and v["hbm"]["frac"] == r["frac"]
