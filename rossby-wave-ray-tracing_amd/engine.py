@@ -272,7 +272,9 @@ class RayEngine:
         key = torch.where(frozen, torch.full_like(work, -1), work)
         return torch.sort(key, descending=True, stable=True).indices.to(torch.int64).contiguous()
 
-    def cost_cell_order(self, st, work, per_octave=2):
+    CELL_PER_OCTAVE = int(os.environ.get("RWRT_CELL_PER_OCTAVE", "2"))   # (env: A/B only)
+
+    def cost_cell_order(self, st, work, per_octave=None):
         """``cost_order`` with spatial locality: rays in coarse cost classes
         (``per_octave`` classes per doubling of the previous launch's work,
         heaviest class first) and, within a class, in Morton order of their
@@ -280,6 +282,7 @@ class RayEngine:
         lines and L2 / MALL sets in their first lookups (the 0.25-degree
         time-varying state of C5 is gathered from HBM: 100 MB per fp64
         level).  Frozen rays last."""
+        per_octave = self.CELL_PER_OCTAVE if per_octave is None else per_octave
         y = st["state"][:5]
         frozen = torch.isnan(y.sum(0))
         w = torch.where(frozen, torch.zeros_like(work), work).to(F64)
