@@ -302,8 +302,9 @@ def main():
                          "cost; C3's default), cost classes then Morton order of the rays' cells (cell; "
                          "C5's default: its lookups are HBM gathers), by all work so far (total), or "
                          "live-first")
-    ap.add_argument("--probe", type=int, default=6,
-                    help="rows of the probe launch over every ray whose attempts split and order the set")
+    ap.add_argument("--probe", type=int, default=None,
+                    help="rows of the probe launch over every ray whose attempts split and order the set "
+                         "(default: 4 for a whole C3 set per GPU, 6 otherwise)")
     ap.add_argument("--first-chunk", default=None,
                     help="rows of the short launches after the probe that re-measure per-ray cost "
                          "(default: C3 on one GPU 24,160 -- profiles/r2/ab/launch_sweep.txt --, "
@@ -342,6 +343,11 @@ def main():
         # (heavy-ray-bound) and C5: 24 + 96
         whole = world == 1 or args.scaling == "weak"
         args.first_chunk = "24,160" if (args.config == "C3" and whole) else "24,96"
+    if args.probe is None:
+        # (profiles/r3/sched/pass_w_schedules.txt: 4 rows +0.75 % over 6 with the
+        # per-launch latency mode, two repetitions each)
+        whole = world == 1 or args.scaling == "weak"
+        args.probe = 4 if (args.config == "C3" and whole) else 6
     if args.team is None:
         # a whole C3 set per GPU: the 160-row launch is bound by its heaviest
         # rays' chains -- 256 of them in latency mode there, 64 in the other
