@@ -353,8 +353,12 @@ def main():
         # rays' chains -- 256 of them in latency mode there, 64 in the other
         # launches (profiles/r3/sched/pass_u_team_per_launch.txt: +0.9 % over
         # none, two repetitions each); a split set: the auto rule
+        # (the non-zonal background: its chain-bound rays are not the predicted
+        # heaviest, and the latency mode's CUs cost 1.5 %: none,
+        # profiles/r3/sched/pass_x_nonzonal_defaults.txt)
         whole = world == 1 or args.scaling == "weak"
-        args.team = "64,256,64" if (args.config == "C3" and whole) else "auto"
+        args.team = (("64,256,64" if args.bg == "zonal" else "0") if (args.config == "C3" and whole)
+                     else "auto")
     if args.lib:
         os.environ["RWRT_LIB"] = os.path.abspath(args.lib)
 
