@@ -212,6 +212,31 @@ def roofline(steps_per_launch, avg_launch_s, workload, schedule, bytes_per_step,
     return out
 
 
+def schedule_defaults(args, world):
+    """The schedule knobs left unset on the command line, by what one GPU
+    holds: a whole C3 set (one GPU, or weak scaling) or a split one / C5.
+      first launches  24 + 160 rows (a whole set: throughput-bound, a longer
+                      second re-ordering launch orders the last one better),
+                      24 + 96 otherwise (profiles/r2/ab/launch_sweep.txt);
+      probe           4 rows for a whole C3 set (+0.75 % over 6 with the
+                      per-launch latency mode, profiles/r3/sched/pass_w_*),
+                      6 otherwise;
+      latency mode    a whole zonal C3 set: 64 / 256 / 64 heaviest rays in the
+                      24- / 160- / rest launches (the 160-row launch is bound
+                      by its heaviest rays' chains; +0.9 %, pass_u_*); a whole
+                      non-zonal set: none (its chain-bound rays are not the
+                      predicted heaviest; 64/256/64 costs 1.5 %, pass_x_*); a
+                      split set: the auto rule (RayEngine.team_size)."""
+    whole = args.config == "C3" and (world == 1 or args.scaling == "weak")
+    if args.first_chunk is None:
+        args.first_chunk = "24,160" if whole else "24,96"
+    if args.probe is None:
+        args.probe = 4 if whole else 6
+    if args.team is None:
+        args.team = ("64,256,64" if args.bg == "zonal" else "0") if whole else "auto"
+    return args
+
+
 def _free_port():
     import socket
     s = socket.socket()
@@ -337,28 +362,7 @@ def main():
     if how == "spawn":
         # no launcher: start the N ranks here, before anything touches the GPU
         return spawn_ranks(world, sys.argv[1:])
-    if args.first_chunk is None:
-        # a whole set on one GPU (throughput-bound): a longer second
-        # re-ordering launch orders the last one better; a split set
-        # (heavy-ray-bound) and C5: 24 + 96
-        whole = world == 1 or args.scaling == "weak"
-        args.first_chunk = "24,160" if (args.config == "C3" and whole) else "24,96"
-    if args.probe is None:
-        # (profiles/r3/sched/pass_w_schedules.txt: 4 rows +0.75 % over 6 with the
-        # per-launch latency mode, two repetitions each)
-        whole = world == 1 or args.scaling == "weak"
-        args.probe = 4 if (args.config == "C3" and whole) else 6
-    if args.team is None:
-        # a whole C3 set per GPU: the 160-row launch is bound by its heaviest
-        # rays' chains -- 256 of them in latency mode there, 64 in the other
-        # launches (profiles/r3/sched/pass_u_team_per_launch.txt: +0.9 % over
-        # none, two repetitions each); a split set: the auto rule
-        # (the non-zonal background: its chain-bound rays are not the predicted
-        # heaviest, and the latency mode's CUs cost 1.5 %: none,
-        # profiles/r3/sched/pass_x_nonzonal_defaults.txt)
-        whole = world == 1 or args.scaling == "weak"
-        args.team = (("64,256,64" if args.bg == "zonal" else "0") if (args.config == "C3" and whole)
-                     else "auto")
+    schedule_defaults(args, world)
     if args.lib:
         os.environ["RWRT_LIB"] = os.path.abspath(args.lib)
 

@@ -82,3 +82,27 @@ def test_roofline_hbm_bound_for_c5(tmp_path):
     assert abs(r["valu_issue"]["frac"] - 1e9 / 0.1 / (1024 * 2.4e9 / 4)) < 1e-9
     v = bench.roofline(1e6, 0.1, "w", [6, 24], 2112, A)
     assert v["bound"] == "valu_issue" and v["hbm"]["frac"] == r["frac"]
+
+
+def test_schedule_defaults():
+    """The bench's schedule defaults by what one GPU holds (a whole C3 set,
+    zonal or not, a split one, C5); explicit values are kept."""
+    import argparse
+    import bench
+
+    def ns(**kw):
+        base = dict(config="C3", scaling="weak", bg="zonal", first_chunk=None, probe=None, team=None)
+        base.update(kw)
+        return argparse.Namespace(**base)
+    a = bench.schedule_defaults(ns(), 1)
+    assert (a.first_chunk, a.probe, a.team) == ("24,160", 4, "64,256,64")
+    a = bench.schedule_defaults(ns(bg="nonzonal"), 8)
+    assert (a.first_chunk, a.probe, a.team) == ("24,160", 4, "0")
+    a = bench.schedule_defaults(ns(scaling="strong"), 8)
+    assert (a.first_chunk, a.probe, a.team) == ("24,96", 6, "auto")
+    a = bench.schedule_defaults(ns(scaling="strong"), 1)
+    assert (a.first_chunk, a.probe, a.team) == ("24,160", 4, "64,256,64")
+    a = bench.schedule_defaults(ns(config="C5"), 1)
+    assert (a.first_chunk, a.probe, a.team) == ("24,96", 6, "auto")
+    a = bench.schedule_defaults(ns(probe=6, team="0", first_chunk="24"), 1)
+    assert (a.first_chunk, a.probe, a.team) == ("24", 6, "0")
