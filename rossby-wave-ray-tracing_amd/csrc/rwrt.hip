@@ -2380,11 +2380,14 @@ __global__ void __launch_bounds__(256, 1) rk45_run_kernel(RunArgs<BG> a) {
     // equals this one: write them all and release the lane.
     const int last = (st == Lane<RayProblem, KStore>::kFrozen) ? a.it_end : it + 1;
     if (!0) {   // (timing-only diagnostic build: no row stores)
+      // non-temporal, like the fill's: the rows stream past the L2 that
+      // holds the basic state (+0.5 % on C3, profiles/r3/sched/pass_aa_nt_rows.txt;
+      // no row stores at all would be +3.3 %)
       double2* o = reinterpret_cast<double2*>(a.out + ((size_t)ray * nrows + (it - a.it_begin)) * RWRT_NOUT);
-      store_row16<0>(o + 0, r0);
-      store_row16<0>(o + 1, r1);
-      store_row16<0>(o + 2, r2);
-      store_row16<0>(o + 3, r3);
+      store_row16<1>(o + 0, r0);
+      store_row16<1>(o + 1, r1);
+      store_row16<1>(o + 2, r2);
+      store_row16<1>(o + 3, r3);
     }
     if (!0 && last > it + 1) {
       asm volatile("");   // frozen: the remaining rows of the chunk (rare branch)

@@ -1,0 +1,14 @@
+#!/bin/bash
+# pass Z (diagnostic): what the frozen-row fill and the live rows' stores cost the step
+set -o pipefail
+O=gpurun_out/r3z
+mkdir -p $O
+b() {
+  timeout -k 10 300 python -u bench.py --no-cpu "$@" > $O/bench.log 2>&1 || { tail -5 $O/bench.log; exit 1; }
+  grep '^{' $O/bench.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('BENCH $*', round(d['value']/1e9,4), round(d['ms_per_step'],1), d['config']['launch_rows'])"
+}
+for rep in 1 2; do
+b || exit 1
+b --lib rossby-wave-ray-tracing_amd/librwrt_nofill.so || exit 1
+b --lib rossby-wave-ray-tracing_amd/librwrt_norows.so || exit 1
+done
