@@ -15,7 +15,9 @@ timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_ACTIV
 cp $out/trace/run_kernel_stats.csv $sum/kernel_stats.csv
 python3 tools/pmc_traffic.py $out/fetch $out/write $out/trace.log $sum/traffic.json
 python3 tools/pmc_valu.py $out/valu $out/trace.log $sum/valu.json
-cp $out/valu/run_counter_collection.csv $sum/valu_counters.csv
+# the run kernel's rows only (the whole collection of a C5 line is ~20 MB)
+python3 -c "import sys; L=open(sys.argv[1]).read().splitlines(); open(sys.argv[2],'w').write('\\n'.join([L[0]]+[l for l in L[1:] if 'rk45_run_kernel' in l])+'\\n')" \
+  $out/valu/run_counter_collection.csv $sum/valu_counters.csv
 grep -h '^{' $out/trace.log > $sum/bench_under_rocprof.json || true
 # keep the summaries only (the raw per-dispatch CSVs of a long run exceed
 # gpurun's 64 MiB merge-back limit)
