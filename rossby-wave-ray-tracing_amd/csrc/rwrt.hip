@@ -54,23 +54,6 @@ __device__ __forceinline__ void store_row16(double2* o, double2 v) {
   }
 }
 
-// The run kernel's row stores: 1 = non-temporal (default), 2 = write-through
-// (the line leaves the XCD's L2 instead of staying in it; A/B variant).
-#ifndef RWRT_ROW_STORE
-#define RWRT_ROW_STORE 1
-#endif
-__device__ __forceinline__ void store_run_row(double2* o, double2 v) {
-#if RWRT_ROW_STORE == 2
-  // the trailing s_nop covers the store-data VGPR hazard (hipcc pads nothing inside asm)
-  v2f64 w;
-  w.x = v.x;
-  w.y = v.y;
-  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" : : "v"(o), "v"(w) : "memory");
-#else
-  store_row16<RWRT_ROW_STORE == 1>(o, v);
-#endif
-}
-
 // Two IEEE f64 divisions qa = a1 / b1, qb = a2 / b2 with the compiler's own
 // instruction sequence (v_div_scale, v_rcp, two Newton steps, v_div_fmas,
 // v_div_fixup: correctly rounded for every input), interleaved by hand.  The
@@ -2401,10 +2384,10 @@ __global__ void __launch_bounds__(256, 1) rk45_run_kernel(RunArgs<BG> a) {
       // holds the basic state (+0.5 % on C3, profiles/r3/sched/pass_aa_nt_rows.txt;
       // no row stores at all would be +3.3 %)
       double2* o = reinterpret_cast<double2*>(a.out + ((size_t)ray * nrows + (it - a.it_begin)) * RWRT_NOUT);
-      store_run_row(o + 0, r0);
-      store_run_row(o + 1, r1);
-      store_run_row(o + 2, r2);
-      store_run_row(o + 3, r3);
+      store_row16<1>(o + 0, r0);
+      store_row16<1>(o + 1, r1);
+      store_row16<1>(o + 2, r2);
+      store_row16<1>(o + 3, r3);
     }
     if (last > it + 1) {
       asm volatile("");   // frozen: the remaining rows of the chunk (rare branch)
