@@ -2292,7 +2292,7 @@ __global__ void __launch_bounds__(256, 1) rk45_run_kernel(RunArgs<BG> a) {
   __shared__ __attribute__((aligned(16))) char smem[kKBytes + LaneBG<BG>::kLdsBytes];
   if constexpr (std::is_same<BG, StaticBG>::value) {
     if ((int)blockIdx.x < a.heavy_blocks) {   // (block-uniform) latency mode
-      if (1) __builtin_amdgcn_s_setprio(1);
+      __builtin_amdgcn_s_setprio(1);
       quad_rays<kTrace>(a, smem + kKBytes, reinterpret_cast<double*>(smem));
       return;
     }
@@ -2305,11 +2305,9 @@ __global__ void __launch_bounds__(256, 1) rk45_run_kernel(RunArgs<BG> a) {
   int64_t ray = -1, nacc = 0, nrej = 0;
   int32_t it = 0, nanrow = 0, wpos = 0;   // (wpos: the ray's queue position, kTrace only)
   double prev_lon = 0.0, prev_lat = 0.0, cos_prev = 0.0;
-  if (1) {
-    // above frozen_fill_kernel's waves (priority 0) sharing the SIMD: the
-    // fill takes the issue cycles the ray loop leaves idle
-    __builtin_amdgcn_s_setprio(1);
-  }
+  // above frozen_fill_kernel's waves (priority 0) sharing the SIMD: the
+  // fill takes the issue cycles the ray loop leaves idle
+  __builtin_amdgcn_s_setprio(1);
   for (;;) {
     if (ray < 0) {
       const int64_t w = a.n_heavy + atomicAdd(&a.queue[1], 1);
