@@ -401,6 +401,15 @@ __device__ __forceinline__ char* lds_slice_base(char* wave_base) {
 // that carry scopes too -- which these (through lds_slice_base) do not.
 __device__ __forceinline__ void lds_dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
+// The static cached lookup reads its cell's LDS slice in this many groups,
+// each group's reads in flight together before its blends.  Two groups (48
+// VGPRs in flight instead of 96) take the run kernel's VGPR spills to AGPRs
+// from 158 to 8: C3 +2.3 % zonal, +1.5 % non-zonal over one group, three
+// groups in between (profiles/r3/sched/pass_ee_cache_read_groups.txt)
+#ifndef RWRT_CACHE_READ_GROUPS
+#define RWRT_CACHE_READ_GROUPS 2
+#endif
+
 struct CachedStaticBG {
   static constexpr bool kTimeVarying = false;
   Field F;
@@ -438,16 +447,21 @@ struct CachedStaticBG {
     k.wb = p.wb;
     k.wc = p.wc;
     k.wd = p.wd;
-    double2 v[4][6];   // every read in flight before the first blend
+    constexpr int kQ = 6 / RWRT_CACHE_READ_GROUPS;
 #pragma unroll
-    for (int q = 0; q < 6; ++q)
+    for (int q0 = 0; q0 < 6; q0 += kQ) {
+      double2 v[4][kQ];   // every read of the group in flight before its first blend
 #pragma unroll
-      for (int j = 0; j < 4; ++j) v[j][q] = chunk(j, q);
-    __builtin_amdgcn_sched_barrier(0);
+      for (int q = 0; q < kQ; ++q)
 #pragma unroll
-    for (int q = 0; q < 6; ++q) {
-      g[2 * q] = blend(k, v[0][q].x, v[1][q].x, v[2][q].x, v[3][q].x);
-      if (2 * q + 1 < 11) g[2 * q + 1] = blend(k, v[0][q].y, v[1][q].y, v[2][q].y, v[3][q].y);
+        for (int j = 0; j < 4; ++j) v[j][q] = chunk(j, q0 + q);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int q = 0; q < kQ; ++q) {
+        const int f = 2 * (q0 + q);
+        g[f] = blend(k, v[0][q].x, v[1][q].x, v[2][q].x, v[3][q].x);
+        if (f + 1 < 11) g[f + 1] = blend(k, v[0][q].y, v[1][q].y, v[2][q].y, v[3][q].y);
+      }
     }
   }
   // Only the RHS looks up through the cache: a lane with |lat| > pi/2 is
@@ -1920,7 +1934,6 @@ struct QuadRole {
 // field is the same blend of the same corner values (bit for bit).
 __device__ __forceinline__ void quad_lookup_end(const CachedStaticBG& B, const QuadRole& R,
                                                 const CachedStaticBG::Pending& p, double g[11]) {
-  static_assert(!0, "quad_lookup_end reads the chunk-major slice layout");
   lds_dma_wait();
   Corners k;
   k.wa = p.wa;
