@@ -9,15 +9,17 @@ days (1081 output rows at 2 h) -- GPU initial rows, solver construction, the
 ray loop and every output row included.  Inputs are resident in HBM when the
 timed region starts.
 
-With N ranks (one per GPU, torch.distributed.run; BASELINE configs[3] = C4)
-the SAME set is split across the GPUs (shard.run_sharded, scaling "strong"):
+With N ranks (one per GPU; BASELINE configs[3] = C4; `--gpus N` starts them,
+or torch.distributed.run does) the SAME set is split across the GPUs
+(shard.run_sharded, scaling "strong", the default):
 inside each timed step rank 0's basic state is broadcast over RCCL, every rank
 builds the initial rows and runs a 6-row probe launch over every ray, the
 probe's per-ray attempts decide a cost-balanced split (no communication: the
 same deterministic rule on every rank), each rank integrates its own rays to
 90 days, and the last row and step counters of every ray are gathered to
 rank 0 over RCCL.  value = the set's accepted ray-steps / the slowest rank's
-wall time.
+wall time.  ``--scaling weak`` (every rank its own C3 set) is a diagnostic:
+its aggregate is reported under ``weak_scaling``, never as ``value``.
 
 Rank 0 prints ONE JSON line.  ``roofline`` prices the ray-loop kernel at the
 bound it actually hits -- VALU instruction issue at one wave per SIMD (PMC
@@ -88,8 +90,11 @@ def make_bs(kind="zonal"):
     return bs, bg
 
 
-def cpu_baseline(bg, y0, nrays, days, seed=0):
-    """Time the oracle on ``nrays`` live rays for ``days`` (1 host core)."""
+def cpu_baseline(bg, y0, nrays, days, seed=0, fsal=True):
+    """Time the oracle on ``nrays`` live rays for ``days`` (1 host core).
+    ``fsal=False``: the reference's loop shape (f recomputed for every column
+    at each step start, rkf45.py:378).  Returns (pick, hist, accepted, seconds,
+    nt, rejected, RHS columns evaluated)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import rwrt_oracle as O
     rng = np.random.default_rng(seed)
@@ -97,11 +102,12 @@ def cpu_baseline(bg, y0, nrays, days, seed=0):
     pick = np.sort(rng.choice(live, size=min(nrays, len(live)), replace=False))
     ob = O.Background(**bg)
     nt = int(round(days * 12)) + 1
+    cols = [0]
     t0 = time.perf_counter()
     with np.errstate(all="ignore"):
-        hist, nacc, nrej, st = O.ray_run(ob, y0[:, pick].copy(), nt, 7200.0)
+        hist, nacc, nrej, st = O.ray_run(ob, y0[:, pick].copy(), nt, 7200.0, fsal=fsal, columns=cols)
     dt = time.perf_counter() - t0
-    return pick, hist, int(nacc.sum()), dt, nt, int(nrej.sum())
+    return pick, hist, int(nacc.sum()), dt, nt, int(nrej.sum()), cols[0]
 
 
 def cpu_baseline_mp(bg, y0, procs, rays_per_proc, days, seed=1):
@@ -115,7 +121,7 @@ def cpu_baseline_mp(bg, y0, procs, rays_per_proc, days, seed=1):
     live = np.where(~np.isnan(y0.mean(axis=0)))[0]
     pick = rng.choice(live, size=min(procs * rays_per_proc, len(live)), replace=False)
     nt = int(round(days * 12)) + 1
-    jobs = [(bg, y0[:, part].copy(), nt, 7200.0) for part in np.array_split(pick, procs)]
+    jobs = [(bg, y0[:, part].copy(), nt, 7200.0, False) for part in np.array_split(pick, procs)]
     with mp.get_context("spawn").Pool(procs) as pool:
         res = pool.map(O.ray_run_timed, jobs)
     steps = sum(r[0] for r in res)
@@ -303,10 +309,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None,
                     help="GPUs (one rank each); without a launcher, N > 1 starts the N ranks itself")
-    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
-                    help="weak: every rank integrates its own full C3 set (the seed grid shifted by "
-                         "rank x 2/N degrees of longitude: N GPUs trace an N-times denser seed grid); "
-                         "strong: ONE C3 set split over the ranks by measured cost (shard.run_sharded)")
+    ap.add_argument("--scaling", default="strong", choices=["weak", "strong"],
+                    help="strong (default; BASELINE configs[3]): ONE C3 set split over the ranks by "
+                         "measured cost (shard.run_sharded).  weak (diagnostic, not a BASELINE config): "
+                         "every rank integrates its own full C3 set (the seed grid shifted by rank x 2/N "
+                         "degrees of longitude) -- reported under 'weak_scaling', never as 'value'")
     ap.add_argument("--dry-run", action="store_true",
                     help="set up the ranks and the process group, print the line's skeleton, stop "
                          "(tests the launcher without a GPU)")
@@ -572,24 +579,35 @@ def main():
                 "rows_per_rank": n_live_max, "bytes": world * n_live_max * 64,
                 "alive_at_end": int(sum(int((~torch.isnan(b[:, 0])).sum().item()) for b in gathered["all"]))}
         if world == 1 and not args.no_cpu:
-            pick, hist, csteps, cdt, cnt, crej = cpu_baseline(bg, y0, args.cpu_rays, args.cpu_days)
-            evals = 6.0 * (csteps + crej) / max(csteps, 1)     # FSAL: 6 RHS columns per attempt
+            pick, hist, csteps, cdt, cnt, crej, ccols = cpu_baseline(bg, y0, args.cpu_rays, args.cpu_days)
+            # the reference's own loop shape, timed on half the sample (the same
+            # rays' first half; ~2x the RHS work per step)
+            rpick, _, rsteps, rdt, _, _, rcols = cpu_baseline(bg, y0, args.cpu_rays // 2, args.cpu_days,
+                                                               seed=2, fsal=False)
             result["cpu_baseline"] = {
-                "value": csteps / cdt, "unit": "ray-steps/s", "cores": 1, "kind": "port",
-                "sample": f"{len(pick)} live C3 rays x {args.cpu_days:g} d ({csteps} ray-steps, "
-                          f"{cdt:.1f} s) with oracle/rwrt_oracle.py: the reference's arithmetic bit for "
-                          f"bit (NumPy), but FSAL -- {evals:.1f} RHS columns per accepted step where the "
-                          f"reference's loop evaluates 14.0 (SURVEY.md 3.3 probe)",
-                "reference_equivalent_value": csteps / cdt * evals / 14.0,
+                "value": rsteps / rdt, "unit": "ray-steps/s", "cores": 1, "kind": "reference_loop",
+                "sample": f"{len(rpick)} live C3 rays x {args.cpu_days:g} d ({rsteps} ray-steps, {rdt:.1f} s) "
+                          f"with oracle/rwrt_oracle.py in the reference's loop shape: f = fun(t, y) "
+                          f"recomputed for every column at each step start (rkf45.py:378) and the rejected "
+                          f"subsets re-run (rkf45.py:410-502) -- {rcols / max(rsteps, 1):.1f} RHS columns per "
+                          f"accepted step; the reference's arithmetic bit for bit (NumPy)",
+                "rhs_columns_per_accepted_step": rcols / max(rsteps, 1),
+                "survey_reference_rate_per_core": "5-6e4 ray-steps/s (BASELINE.md; SURVEY.md 8(d), the "
+                                                  "reference itself on the survey host)",
+                "port_fsal": {"value": csteps / cdt, "unit": "ray-steps/s", "cores": 1, "kind": "port",
+                              "sample": f"{len(pick)} live C3 rays x {args.cpu_days:g} d ({csteps} ray-steps, "
+                                        f"{cdt:.1f} s), FSAL: {ccols / max(csteps, 1):.1f} RHS columns per "
+                                        f"accepted step"},
                 "host_cpus": os.cpu_count()}
             if args.cpu_procs > 1:
-                msteps, mwall, mrays = cpu_baseline_mp(bg, y0, args.cpu_procs, args.cpu_rays // 4,
+                msteps, mwall, mrays = cpu_baseline_mp(bg, y0, args.cpu_procs, args.cpu_rays // 8,
                                                        args.cpu_days)
                 result["cpu_baseline_mp"] = {
                     "value": msteps / mwall, "unit": "ray-steps/s", "cores": args.cpu_procs,
-                    "kind": "port",
+                    "kind": "reference_loop",
                     "sample": f"{mrays} live C3 rays x {args.cpu_days:g} d over {args.cpu_procs} "
-                              f"processes ({msteps} ray-steps, slowest process {mwall:.1f} s)"}
+                              f"processes in the reference's loop shape ({msteps} ray-steps, slowest "
+                              f"process {mwall:.1f} s)"}
             # parity of the same sample on the GPU after the same horizon
             rows = {}
             eng.integrate(torch.as_tensor(y0[:, pick], device=dev), cnt, 7200.0,
@@ -612,6 +630,13 @@ def main():
                 "identical_values_frac": float(same.mean()),
                 "rays_identical_all_rows": int(same.all(axis=(0, 1)).sum()),
                 "note": "GPU rows vs the oracle (NumPy, the reference's arithmetic) on the cpu_baseline sample"}
+        if weak:
+            # not a BASELINE config (N x the C3 set): the aggregate rides under
+            # its own key; the line's value stays empty
+            result["weak_scaling"] = {"value": value, "unit": "ray-steps/s",
+                                      "note": f"{world} x the C3 set (each rank its own seed grid); "
+                                              "a diagnostic of per-GPU throughput, not BASELINE configs[3]"}
+            result["value"] = None
         print(json.dumps(result))
     if dist:
         dist.barrier()
@@ -760,7 +785,7 @@ def main_c5(args, dist, group, rank, world, dev, share=1):
         torch.cuda.empty_cache()
         parity = c5_parity_sample(eng, torch.cat([x.reshape(7, -1) for x in rows], dim=1), args.fields, dev) \
             if args.days >= 10 else {"skipped": "needs --days >= 10 (the fixture's horizon)"}
-        print(json.dumps({
+        c5_line = {
             "metric": METRIC, "value": tot_steps / max_el, "unit": "ray-steps/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * max_el / args.steps,
             "higher_is_better": True, "scaling": "weak" if weak else "strong", "vs_baseline": None,
@@ -779,7 +804,12 @@ def main_c5(args, dist, group, rank, world, dev, share=1):
             "queue_order": args.order,
             "library_sha256": library_sha(),
             "init": "GPU rwrt_ray_initial inside every timed step",
-            "roofline": roofline(per_launch_steps, avg_launch_s, workload, schedule, bps, args, bound="hbm")}))
+            "roofline": roofline(per_launch_steps, avg_launch_s, workload, schedule, bps, args, bound="hbm")}
+        if weak and world > 1:
+            c5_line["weak_scaling"] = {"value": c5_line["value"], "unit": "ray-steps/s",
+                                       "note": f"{world} x the C5 set: a diagnostic, not BASELINE configs[4]"}
+            c5_line["value"] = None
+        print(json.dumps(c5_line))
     if dist:
         dist.barrier()
         dist.destroy_process_group()

@@ -511,15 +511,26 @@ def cal_dis(lon_c, lat_c, lon_p, lat_p):
 
 
 def ray_run(bg, y0, nt, tstep, rtol=1e-6, atol=1e-6, msf=1e-3, cut_off=0.1,
-            ttotal=None, row0=None):
+            ttotal=None, row0=None, fsal=True, columns=None):
     """Integrate rays ``y0[5, nray]`` -> history ``hist[7, nt, nray]`` (rows 1.. filled).
 
     Row 0 of ``hist`` is ``row0[7, nray]`` when given (the ``ray_initial`` rows),
     else ``y0`` with NaN ``ug, vg``.  Returns ``(hist, nacc, nrej, status)``;
     ``status`` is 0, or -1 when the solver failed (remaining rows NaN,
     wr.py:886-887).
+
+    ``fsal=False`` runs the reference's own loop shape: ``f = fun(t, y)``
+    recomputed for EVERY column at each step start (rkf45.py:378, frozen and
+    finished columns included) besides the rejected subsets' re-runs
+    (rkf45.py:410-502) -- the same values (the RHS is autonomous: f is K6 bit
+    for bit), about twice the RHS columns; bench.py times it as the
+    reference-structured CPU baseline.  ``columns`` (a one-element list, if
+    given) accumulates the RHS columns evaluated.
     """
-    fun = lambda t, y: rhs(bg, y, t)[0]   # FSAL (DP54 autonomous=True) for both backgrounds
+    def fun(t, y):
+        if columns is not None:
+            columns[0] += y.shape[-1]
+        return rhs(bg, y, t)[0]
     nray = y0.shape[1]
     hist = np.full((7, nt, nray), np.nan)
     if row0 is not None:
@@ -531,7 +542,7 @@ def ray_run(bg, y0, nt, tstep, rtol=1e-6, atol=1e-6, msf=1e-3, cut_off=0.1,
         t_eval[-1] = ttotal
     cut = cut_off * tstep / 3600.0                                     # wr.py:170
     try:
-        sol = DP54(fun, 0, y0, tstep, rtol, atol, msf * tstep)
+        sol = DP54(fun, 0, y0, tstep, rtol, atol, msf * tstep, autonomous=fsal)
     except SolverFailed:
         return hist, np.zeros(nray, np.int64), np.zeros(nray, np.int64), -1
     for i in range(1, nt):
@@ -654,7 +665,7 @@ def source_matrix(SW_lon, SW_lat, dlon, dlat, nnx, nny):
     return lon, lat
 
 
-def run_config(bg, cfg, nt=None):
+def run_config(bg, cfg, nt=None, **kw):
     """End-to-end oracle of ``real2d_hnf`` for a ``synthetic.SeedConfig``."""
     slon, slat = source_matrix(cfg.SW_lon, cfg.SW_lat, cfg.dlon, cfg.dlat, cfg.nnx, cfg.nny)
     rows = ray_initial(bg, slon, slat, cfg.zwn, cfg.freq)
@@ -664,7 +675,7 @@ def run_config(bg, cfg, nt=None):
     y0 = np.array(rows[:5]).reshape(5, -1)
     row0 = np.array(rows).reshape(7, -1)
     return ray_run(bg, y0, nt, tstep, cfg.rtol, cfg.atol, cfg.MinStepFactor,
-                   ttotal=cfg.ttotal * DAY, row0=row0)
+                   ttotal=cfg.ttotal * DAY, row0=row0, **kw)
 
 
 # ----------------------------------------------------------------------------
@@ -745,9 +756,10 @@ def ray_run_timed(args):
     one process of bench.py's multi-core CPU baseline (picklable, imports
     nothing beyond this module)."""
     import time
-    bg_kwargs, y0, nt, tstep = args
+    bg_kwargs, y0, nt, tstep = args[:4]
+    fsal = args[4] if len(args) > 4 else True
     bg = Background(**bg_kwargs)
     t0 = time.perf_counter()
     with np.errstate(all="ignore"):
-        _, nacc, _, _ = ray_run(bg, y0, nt, tstep)
+        _, nacc, _, _ = ray_run(bg, y0, nt, tstep, fsal=fsal)
     return int(nacc.sum()), time.perf_counter() - t0

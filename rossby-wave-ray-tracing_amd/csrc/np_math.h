@@ -54,7 +54,10 @@ namespace np_math {
 #endif
 NM_FN double nm_d(unsigned long long u) { return NM_KVAL(u); }
 NM_FN unsigned long long nm_u(double x) { return __builtin_bit_cast(unsigned long long, x); }
-NM_FN double nm_fma(double a, double b, double c) { return __builtin_fma(a, b, c); }
+#ifndef NM_FMA
+#define NM_FMA(a, b, c) __builtin_fma((a), (b), (c))
+#endif
+NM_FN double nm_fma(double a, double b, double c) { return NM_FMA(a, b, c); }
 NM_FN double nm_abs(double x) { return nm_d(nm_u(x) & 0x7FFFFFFFFFFFFFFFull); }
 NM_FN double nm_sign(double x) { return nm_d(nm_u(x) & 0x8000000000000000ull); }
 NM_FN double nm_copysign(double m, double s) {
@@ -77,6 +80,11 @@ NM_FN double nm_copysign(double m, double s) {
 // (e.g. a scheduling barrier); nothing on the host
 #ifndef NM_ISSUE_FENCE
 #define NM_ISSUE_FENCE()
+#endif
+// NM_RARE(c): the condition of a rarely taken branch (an includer's static
+// analysis build may compile those branches away; default: the condition)
+#ifndef NM_RARE
+#define NM_RARE(c) (c)
 #endif
 
 // ---------------------------------------------------------------------------
@@ -192,12 +200,15 @@ NM_FN double nm_sin(double x) {
     const double t = nm_d(kG_HP0) - nm_abs(x);
     return nm_copysign(g_do_cos(t, nm_d(kG_HP1)), x);
   }
-  if (k < 0x419921FBu) {                                      // |x| < 105414350
-    double a, da;
-    const int n = g_reduce(x, a, da);
-    return g_do_sincos(a, da, n);
+  if (NM_RARE(true)) {                                        // |x| >= 2.426265 (rare)
+    if (k < 0x419921FBu) {                                    // |x| < 105414350
+      double a, da;
+      const int n = g_reduce(x, a, da);
+      return g_do_sincos(a, da, n);
+    }
+    return NM_FALLBACK_SIN(x);
   }
-  return NM_FALLBACK_SIN(x);
+  return x;   // (not reached)
 }
 
 NM_FN double nm_cos(double x) {
@@ -210,12 +221,15 @@ NM_FN double nm_cos(double x) {
     const double da = (y - a) + nm_d(kG_HP1);
     return g_do_sin(a, da);
   }
-  if (k < 0x419921FBu) {
-    double a, da;
-    const int n = g_reduce(x, a, da);
-    return g_do_sincos(a, da, n + 1);
+  if (NM_RARE(true)) {                                        // |x| >= 2.426265 (rare)
+    if (k < 0x419921FBu) {
+      double a, da;
+      const int n = g_reduce(x, a, da);
+      return g_do_sincos(a, da, n + 1);
+    }
+    return NM_FALLBACK_COS(x);
   }
-  return NM_FALLBACK_COS(x);
+  return x;   // (not reached)
 }
 
 // sin and cos of one argument, bit for bit nm_sin(x) and nm_cos(x), with the
@@ -257,7 +271,7 @@ NM_FN void nm_sincos_main(double x, double& sn, double& cs) {
 NM_FN bool nm_sincos_rare(double x) { return !(g_hi(x) < 0x400368FDu); }
 NM_FN void nm_sincos(double x, double& sn, double& cs) {
   nm_sincos_main(x, sn, cs);
-  if (nm_sincos_rare(x)) {                                    // |x| >= 2.426265, inf, NaN (rare)
+  if (NM_RARE(nm_sincos_rare(x))) {                                    // |x| >= 2.426265, inf, NaN (rare)
     sn = nm_sin(x);
     cs = nm_cos(x);
   }
@@ -343,7 +357,7 @@ NM_FN void nm_sincostan(double x, double& sn, double& cs, double& tn) {
   NM_ISSUE_FENCE();
   nm_sincos_fin(x, P, sn, cs);
   tn = nm_tan_fin(tp, A, Nk);
-  if (nm_sincos_rare(x)) {                                    // |x| >= 2.426265, inf, NaN (rare)
+  if (NM_RARE(nm_sincos_rare(x))) {                                    // |x| >= 2.426265, inf, NaN (rare)
     sn = nm_sin(x);
     cs = nm_cos(x);
     tn = nm_tan(x);
@@ -373,7 +387,7 @@ NM_FN SinCosTanPre nm_sincostan_begin(double x) {
 NM_FN void nm_sincostan_end(double x, const SinCosTanPre& r, double& sn, double& cs, double& tn) {
   nm_sincos_fin(x, r.P, sn, cs);
   tn = nm_tan_fin(r.tp, r.A, r.Nk);
-  if (nm_sincos_rare(x)) {                                    // |x| >= 2.426265, inf, NaN (rare)
+  if (NM_RARE(nm_sincos_rare(x))) {                                    // |x| >= 2.426265, inf, NaN (rare)
     sn = nm_sin(x);
     cs = nm_cos(x);
     tn = nm_tan(x);
@@ -489,8 +503,8 @@ NM_FN double nm_pow(double x, double y) {
   p1 = nm_fma(Eh, p1, Eh);
   const double scale = nm_d((unsigned long long)(kk + 1023) << 52);
   const double v = p1 * scale;
-  if (xs || ys) return nm_pow_special(x, y);
-  if (ovf) return NM_FALLBACK_POW(x, y);
+  if (NM_RARE(xs || ys)) return nm_pow_special(x, y);
+  if (NM_RARE(ovf)) return NM_FALLBACK_POW(x, y);
   return v;
 }
 

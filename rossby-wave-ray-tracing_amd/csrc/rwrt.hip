@@ -25,6 +25,21 @@
 #include "rwrt.h"
 #include "nproots.h"
 
+// RARE(c): the condition of a rarely taken branch.  The static analysis build
+// (-DRWRT_ANALYZE_HOT, tools/hot_count.py; never loaded) compiles those branches
+// away so that the run kernel's loop is its common path, straight-line, and
+// its static instruction count is the dynamic count of an attempt.
+#ifdef RWRT_ANALYZE_HOT
+// (the condition is still computed: its lane mask is consumed by an empty asm)
+__device__ __forceinline__ bool rwrt_rare_sink(bool c) {
+  asm volatile("; rare %0" ::"s"(__builtin_amdgcn_ballot_w64(c)));
+  return false;
+}
+#define RARE(c) rwrt_rare_sink(c)
+#else
+#define RARE(c) (c)
+#endif
+
 namespace rwrt {
 
 // constants.py:13-16
@@ -144,7 +159,7 @@ __device__ __forceinline__ double fmod_pos(double a, double b, double binv = 0.0
   double r = fma(-n, b, x);
   const double lo = r + b, hi = fma(-(n + 1.0), b, x);
   r = (r < 0.0) ? lo : ((r >= b) ? hi : r);
-  if (!(x < 0x1p40)) {
+  if (RARE(!(x < 0x1p40))) {
     asm volatile("");   // NaN, inf, huge: library routine (rare branch)
     r = fabs(fmod(a, b));
   }
@@ -207,7 +222,7 @@ __device__ __forceinline__ double div_hw(double a, double b, double rb) {
   double r = copysign(fma(rem, rb, q), q);
   const double aa = fabs(a);
   const bool bad = !(aa < 0x1p600) | ((aa < 0x1p-900) & (aa != 0.0)) | (rb == 0.0);
-  if (bad) {
+  if (RARE(bad)) {
     asm volatile("");   // keep the IEEE division on its (rarely taken) branch
     r = a / b;
   }
@@ -409,6 +424,8 @@ __device__ __forceinline__ void lds_dma_wait() { asm volatile("s_waitcnt vmcnt(0
 #ifndef RWRT_CACHE_READ_GROUPS
 #define RWRT_CACHE_READ_GROUPS 2
 #endif
+static_assert(RWRT_CACHE_READ_GROUPS >= 1 && 6 % RWRT_CACHE_READ_GROUPS == 0,
+              "RWRT_CACHE_READ_GROUPS must divide the 6 chunks of a record (1, 2, 3 or 6)");
 
 struct CachedStaticBG {
   static constexpr bool kTimeVarying = false;
@@ -873,6 +890,7 @@ __device__ __forceinline__ double add_rd(double a, double b) {
 #define NM_ADD_RZ(a, b) ::rwrt::add_rz((a), (b))
 #define NM_ADD_RD(a, b) ::rwrt::add_rd((a), (b))
 #define NM_ISSUE_FENCE() __builtin_amdgcn_sched_barrier(0)
+#define NM_RARE(c) RARE(c)
 #define NM_FALLBACK_SIN(x) ::sin(x)
 #define NM_FALLBACK_COS(x) ::cos(x)
 #define NM_FALLBACK_TAN(x) ::tan(x)
@@ -991,7 +1009,7 @@ __device__ __forceinline__ void mercator12(const double g[11], const Merc& M, do
   o[10] = g[F_QXY] * cp;
   o[9] = o[10];
   o[11] = ((g[F_QYY] * cp) - (g[F_QY] * M.s)) * cp;
-  if (M.m != 1.0) {
+  if (RARE(M.m != 1.0)) {
     asm volatile("");   // keep the masked recomputation on its (rarely taken) branch
     mercator12_masked(g, M, t, o);
   }
@@ -1193,7 +1211,7 @@ __device__ __forceinline__ void ray_rhs(const BG& B, double t, const double* y, 
   lookup_end(B, pending, g);
   const Merc M = merc_factors(lat, c, s);
   double ug, vg;
-  if (!rhs_tail_fast(g, M, s, c, tn, kx, kw, G, amp, dy, ug, vg)) {
+  if (RARE(!rhs_tail_fast(g, M, s, c, tn, kx, kw, G, amp, dy, ug, vg))) {
     asm volatile("");   // an operand outside qdiv's exact range, or the pole band (rare branch)
     rhs_tail_ieee(g, M, s, c, tn, kx, ky, amp, dy, ug, vg);
   }
@@ -1333,7 +1351,7 @@ __device__ __forceinline__ bool cal_dis_reaches(double lon_c, double lat_c, doub
   sin2((lat_c - lat_p) / 2.0, (lon_c - lon_p) / 2.0, sd, sl);
   const double a = sd * sd + (cos_p * cos_c) * (sl * sl);
   bool r = false;
-  if (!(a < cut_a)) {
+  if (RARE(!(a < cut_a))) {
     asm volatile("");   // rare: near or past the threshold, or NaN
     r = fabs(2.0 * atan2(sqrt(a), sqrt(1.0 - a))) >= cut_off;
   }
@@ -2304,7 +2322,7 @@ __global__ void __launch_bounds__(256, 1) rk45_run_kernel(RunArgs<BG> a) {
   constexpr int kKBytes = 5 * 5 * 256 * 8;
   __shared__ __attribute__((aligned(16))) char smem[kKBytes + LaneBG<BG>::kLdsBytes];
   if constexpr (std::is_same<BG, StaticBG>::value) {
-    if ((int)blockIdx.x < a.heavy_blocks) {   // (block-uniform) latency mode
+    if (RARE((int)blockIdx.x < a.heavy_blocks)) {   // (block-uniform) latency mode
       __builtin_amdgcn_s_setprio(1);
       quad_rays<kTrace>(a, smem + kKBytes, reinterpret_cast<double*>(smem));
       return;
@@ -2381,7 +2399,7 @@ __global__ void __launch_bounds__(256, 1) rk45_run_kernel(RunArgs<BG> a) {
     } else if (have) {
       ug = L.aux[0];
       vg = L.aux[1];
-    } else {
+    } else if (RARE(true)) {   // the last evaluation at y was masked (rare)
       ugvg_at(a.B, tb, y[0], y[1], y[2], y[3], ug, vg);
     }
     const double2 r0 = make_double2(y[0], y[1]), r1 = make_double2(y[2], y[3]);
@@ -2400,7 +2418,7 @@ __global__ void __launch_bounds__(256, 1) rk45_run_kernel(RunArgs<BG> a) {
       store_row16<1>(o + 2, r2);
       store_row16<1>(o + 3, r3);
     }
-    if (last > it + 1) {
+    if (RARE(last > it + 1)) {
       asm volatile("");   // frozen: the remaining rows of the chunk (rare branch)
       for (int k = it + 1; k < last; ++k) {
         double2* o = reinterpret_cast<double2*>(a.out + ((size_t)ray * nrows + (k - a.it_begin)) * RWRT_NOUT);
@@ -2557,6 +2575,7 @@ __global__ void math_kernel(int kind, int64_t n, const double* __restrict__ x,
     case 9: { double sn, cs; sincos(a, &sn, &cs); r = sn; } break;
     case 10: { double sn, cs; sincos(a, &sn, &cs); r = cs; } break;
     case 11: r = div_rearth(a); break;
+    case 12: r = fmod_pos(a, b); break;
     case 13: r = py_mod_2pi(a); break;
     case 14: r = py_mod_2pi_again(py_mod_2pi(a)); break;
     case 15: r = div_hw(a, b, recip_hw(b)); break;
@@ -2579,7 +2598,7 @@ __global__ void math_kernel(int kind, int64_t n, const double* __restrict__ x,
       G.den(b);
       r = G.ok() ? 1.0 : 0.0;
     } break;
-    default: r = fmod_pos(a, b); break;
+    default: r = kNaN; break;   // (unreachable: rwrt_selftest_math rejects other kinds)
   }
   out[i] = r;
 }
@@ -3130,9 +3149,8 @@ rwrt_status launch_run(rwrt_ctx* ctx, const BG& B, int64_t nray, const rwrt_para
     }
     if (rwrt_status s = check_launch("rk45_run_kernel")) return s;
   }
-  if (0 != 1)
-    hipLaunchKernelGGL(frozen_fill_kernel<BG>, dim3((unsigned)((nray + kFillThreads - 1) / kFillThreads)),
-                       dim3(kFillThreads), 0, 0 == 2 ? st : ctx->side, a);
+  hipLaunchKernelGGL(frozen_fill_kernel<BG>, dim3((unsigned)((nray + kFillThreads - 1) / kFillThreads)),
+                     dim3(kFillThreads), 0, ctx->side, a);
   if (rwrt_status s = check_launch("frozen_fill_kernel")) return s;
   return ctx_end(ctx, st);
 }
@@ -3586,6 +3604,8 @@ rwrt_status rwrt_selftest_math(int32_t kind, int64_t n, const double* d_x, const
                                double* d_out, void* stream) {
   if (n < 0 || kind < 0 || kind > 35 || (n > 0 && (!d_x || !d_out)))
     return fail(RWRT_ERR_ARG, "bad selftest arguments%s");
+  if (kind >= 17 && kind <= 22)   // retired device-libm restatements: never alias another kind
+    return fail(RWRT_ERR_ARG, "selftest kinds 17-22 are retired%s");
   if (n == 0) return RWRT_OK;
   hipLaunchKernelGGL(math_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, kind,
                      n, d_x, d_y, d_out);

@@ -47,6 +47,18 @@ def test_argument_errors_are_reported_without_a_gpu():
     assert st == H.RWRT_ERR_ARG and b"rwrt_ctx" in lib.rwrt_last_error()
 
 
+def test_selftest_kinds_retired_are_errors():
+    """Retired selftest kinds (17-22) are refused instead of aliasing another
+    operation; a live kind with n = 0 is a no-op (no GPU needed)."""
+    lib = H.load()
+    for kind in range(17, 23):
+        assert lib.rwrt_selftest_math(kind, 0, None, None, None, None) == H.RWRT_ERR_ARG
+        assert b"retired" in lib.rwrt_last_error()
+    for kind in (0, 12, 16, 23, 35):
+        assert lib.rwrt_selftest_math(kind, 0, None, None, None, None) == H.RWRT_OK
+    assert lib.rwrt_selftest_math(36, 0, None, None, None, None) == H.RWRT_ERR_ARG
+
+
 def test_context_needs_a_device():
     """rwrt_ctx_create refuses a device that does not exist (none on the build
     host); destroying NULL is a no-op."""

@@ -46,7 +46,16 @@ def test_gpus2_spawns_two_ranks_one_line():
     assert len(lines) == 1, p.stdout                # rank 0 alone prints
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["world_sum"] == 2.0 and d["backend"] == "gloo"
-    assert d["scaling"] == "weak"
+    # the default N > 1 run is BASELINE configs[3]: ONE C3 set split over the
+    # ranks (strong scaling); weak scaling is an explicit, separately keyed
+    # diagnostic
+    assert d["scaling"] == "strong"
+
+
+def test_weak_scaling_is_opt_in():
+    p, lines = _bench(["--gpus", "2", "--dry-run", "--scaling", "weak"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert json.loads(lines[0])["scaling"] == "weak"
 
 
 def test_gpus_mismatch_under_launcher_fails_loudly():

@@ -29,9 +29,10 @@ from make_devmath import row_hashes  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 
-def run_c3_90d(kind, team="auto"):
+def run_c3_90d(kind, team="auto", probe=6, split=None, info=None):
     """Rows [7, 1081, n] and (nacc, nrej) of the fixture's sample, from a
-    full-set 90-day run with the bench's schedule."""
+    full-set 90-day run with the bench's schedule.  ``info`` (a dict, if given)
+    receives the engine's long-launch split decision."""
     import torch
     from bench import c3_sources, make_bs
     from engine import RayEngine
@@ -57,8 +58,10 @@ def run_c3_90d(kind, team="auto"):
         got = rows[m][:, :, :7].cpu().numpy()          # (k, i1 - i0, 7)
         hist[:, i0:i1, p[m].cpu().numpy()] = np.transpose(got, (2, 1, 0))
 
-    r = run_sharded(eng, rows0[:5].contiguous(), nt, 7200.0, rank=0, world=1, probe=6, lead=[24, 160],
-                    chunk=nt - 1, sink=sink, ttotal=(nt - 1) * 7200.0, team=team)
+    r = run_sharded(eng, rows0[:5].contiguous(), nt, 7200.0, rank=0, world=1, probe=probe, lead=[24, 160],
+                    chunk=nt - 1, sink=sink, ttotal=(nt - 1) * 7200.0, team=team, split=split)
+    if info is not None:
+        info.update(split_rho=eng.split_rho, threshold=eng.SPLIT_RHO, bounds=list(r.res.bounds))
     counts = torch.empty((rows0.shape[1], 2), dtype=torch.int64, device=eng.device)
     counts[r.idx] = r.counts
     counts = counts[idx].cpu().numpy()
@@ -82,8 +85,16 @@ def check(g, hist, counts):
 
 @pytest.mark.parametrize("kind", ["zonal", "nonzonal"])
 def test_c3_90d_sample_bitwise_with_reference_arithmetic(kind):
-    g, hist, counts = run_c3_90d(kind)
+    """The bench's own schedule for a whole set (bench.schedule_defaults: a
+    4-row probe, 24 + 160 rows, the adaptive split of the long launch; latency
+    mode 64 / 256 / 64 on the zonal jets, none on the non-zonal set, where the
+    split must actually happen)."""
+    info = {}
+    g, hist, counts = run_c3_90d(kind, team=[64, 256, 64] if kind == "zonal" else 0, probe=4, split="auto",
+                                 info=info)
     check(g, hist, counts)
+    if kind == "nonzonal":
+        assert info["split_rho"] is not None and info["split_rho"] < info["threshold"], info
     # the sample is what it claims: the heaviest rays of the set, alive at 90 d
     assert int(g["cost90"].max()) == int(counts.sum(1).max()) and counts.sum(1).max() > 10000
     assert int((~np.isnan(hist[0, -1])).sum()) > hist.shape[2] // 2

@@ -62,7 +62,8 @@ def test_c5_10d_41_levels_bitwise_with_oracle(storage):
 
     chunk = 240 if lv.fp32 else 48          # bench.py main_c5's rows per launch
     r = run_sharded(eng, rows0[:5].contiguous(), nt, 7200.0, rank=0, world=1, probe=6, lead=[24, 96],
-                    chunk=chunk, sink=sink, ttotal=(nt - 1) * 7200.0)
+                    chunk=chunk, sink=sink, ttotal=(nt - 1) * 7200.0,
+                    order_policy="cell")   # bench.py's C5 default queue order
     counts = r.counts[idx].cpu().numpy()
     del eng, lv, r
     torch.cuda.empty_cache()

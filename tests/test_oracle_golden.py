@@ -109,6 +109,23 @@ def test_c1_trajectory_bitwise():
 
 
 @pytest.mark.parametrize("kind", KINDS)
+def test_reference_loop_shape_bitwise(kind):
+    """The oracle's reference-structured loop (f recomputed for every column at
+    each step start, rkf45.py:378; bench.py's cpu_baseline) gives the same
+    bits as the FSAL loop, and evaluates the RHS on about twice the columns."""
+    g = golden(f"traj_C2_{kind}.npz")
+    cols = [0]
+    with np.errstate(all="ignore"):
+        hist, nacc, nrej, st = O.run_config(bg(kind), S.config("C2"), nt=13, fsal=False, columns=cols)
+        h2, nacc2, _, _ = O.run_config(bg(kind), S.config("C2"), nt=13)
+    assert st == 0
+    assert same(hist, h2) and same(nacc, nacc2)
+    assert same(hist[:, 1], g["hist"][:, 0]) and same(hist[:, 12], g["hist"][:, 1])
+    per_acc = cols[0] / nacc.sum()
+    assert 10.0 < per_acc < 30.0, per_acc
+
+
+@pytest.mark.parametrize("kind", KINDS)
 def test_c2_trajectory_bitwise(kind):
     g = golden(f"traj_C2_{kind}.npz")
     with np.errstate(all="ignore"):
