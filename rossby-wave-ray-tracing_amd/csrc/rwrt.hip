@@ -253,6 +253,7 @@ struct Corners {
   const double* d;  // F[x1, y0]
   double wa, wb, wc, wd;
   unsigned key_x, key_y;   // x0 | x1 << 16, y0 | y1 << 16 (W, H < 2^16)
+  unsigned pa, pb, pc, pd; // grid-point indices x * H + y of a, b, c, d
   unsigned oa, ob, oc, od; // element offsets of a, b, c, d from F.P
 };
 
@@ -269,10 +270,14 @@ __device__ __forceinline__ Corners corners(const Field& F, double lon, double la
   // (W, H < 2^24: 24-bit multiplies)
   const unsigned c0 = __umul24(x0, F.H), c1 = __umul24(x1, F.H);
   Corners k;
-  k.oa = __umul24(c0 + y1, kNF);
-  k.ob = __umul24(c1 + y1, kNF);
-  k.oc = __umul24(c0 + y0, kNF);
-  k.od = __umul24(c1 + y0, kNF);
+  k.pa = c0 + y1;
+  k.pb = c1 + y1;
+  k.pc = c0 + y0;
+  k.pd = c1 + y0;
+  k.oa = __umul24(k.pa, kNF);
+  k.ob = __umul24(k.pb, kNF);
+  k.oc = __umul24(k.pc, kNF);
+  k.od = __umul24(k.pd, kNF);
   k.a = F.P + k.oa;
   k.b = F.P + k.ob;
   k.c = F.P + k.oc;
@@ -353,6 +358,7 @@ __device__ __forceinline__ void interp4(const Field& F, double lon, double lat,
 struct StaticBG {
   static constexpr bool kTimeVarying = false;
   Field F;
+  const char* img = nullptr;   // cache image of F (cache_image_kernel; the run kernels' refills)
   __device__ __forceinline__ void interp11(double lon, double lat, double, double g[11]) const {
     rwrt::interp11(F, py_mod_2pi(lon), lat, g);
   }
@@ -427,10 +433,37 @@ __device__ __forceinline__ void lds_dma_wait() { asm volatile("s_waitcnt vmcnt(0
 static_assert(RWRT_CACHE_READ_GROUPS >= 1 && 6 % RWRT_CACHE_READ_GROUPS == 0,
               "RWRT_CACHE_READ_GROUPS must divide the 6 chunks of a record (1, 2, 3 or 6)");
 
+// The cache image of the static state: the records of 64 consecutive grid
+// points stored chunk-major, so that a corner's six 16-B chunks lie 1 KiB
+// apart in global memory exactly as in the LDS slice (where one LDS-DMA
+// instruction writes its 64 lanes' 16 B as 1 KiB):
+//   chunk q of point p at (p >> 6) * 6 KiB + q * 1 KiB + (p & 63) * 16 B.
+// A refill then addresses each corner ONCE (a 32-bit offset from the image
+// base) and its chunks by the instruction's immediate offset, which the
+// hardware adds to the global and to the LDS address alike: per refill 4
+// corner offsets and 8 M0 values instead of 24 64-bit addresses and 24 M0
+// values.  Built per launch from the packed state (cache_image_kernel, ~1 MB
+// at 2.5 degrees, the context's scratch).
+constexpr unsigned kImgTile = 6 * 1024;
+inline size_t cache_image_bytes(int64_t npts) { return (size_t)((npts + 63) / 64) * kImgTile; }
+// (= p * 16 + (p >> 6) * 5 KiB: a shift, a 24-bit multiply, a shift-add)
+__device__ __forceinline__ unsigned img_offset(unsigned p) { return __umul24(p >> 6, kImgTile - 1024u) + p * 16u; }
+
+__global__ void cache_image_kernel(Field F, char* __restrict__ img) {
+  const int64_t n = (int64_t)F.W * F.H * 6;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const unsigned p = (unsigned)(i / 6), q = (unsigned)(i - (int64_t)p * 6);
+    const double2 v = reinterpret_cast<const double2*>(F.P + (size_t)p * kNF)[q];
+    *reinterpret_cast<double2*>(img + img_offset(p) + q * 1024u) = v;
+  }
+}
+
 struct CachedStaticBG {
   static constexpr bool kTimeVarying = false;
   Field F;
+  const char* img;                // cache image of F (global)
   char* wave_base;                // this wave's slice area (wave-uniform)
+  const char* img_hi;             // img + 4 KiB, kept in its own SGPR pair (the refill's chunks 4-5)
   unsigned lane16;                // lane * 16
   mutable unsigned key_x, key_y;  // cell held in the slice (~0u: none)
 
@@ -440,18 +473,86 @@ struct CachedStaticBG {
   __device__ __forceinline__ const double2& chunk(int j, int q) const {
     return *reinterpret_cast<const double2*>(wave_base + (j * 6 + q) * 1024 + lane16);
   }
+  // The 24 LDS-DMA loads of a refill (corner j's chunks from image offset oj
+  // into the slice at j * 6 KiB), in ONE asm statement that sets M0 itself
+  // (M0 is compiler-reserved: saved and restored here).  Issued behind the
+  // compiler's back on purpose: an LDS-DMA the compiler knows of makes it
+  // wait for EVERY outstanding LDS read (lgkmcnt(0)) before the first use of
+  // any -- the cell cache's reads in end() would all have to land before the
+  // first blend; unaware of the DMA it waits per read (lgkmcnt(N)).  end()
+  // waits for the DMA explicitly (lds_dma_wait), as before.
+  __device__ __forceinline__ void refill(unsigned o0, unsigned o1, unsigned o2, unsigned o3) const {
+    typedef __attribute__((address_space(3))) char lds_char;
+    const unsigned l = (unsigned)(size_t)(lds_char*)wave_base;
+    unsigned keep;
+#define RWRT_REFILL_CORNER(O, LOFF, LOFF4)                                        \
+    "s_add_u32 m0, %[l], " #LOFF "\n\t"                                          \
+    "s_nop 0\n\t"                                                               \
+    "global_load_lds_dwordx4 %[" #O "], %[g0]\n\t"                              \
+    "global_load_lds_dwordx4 %[" #O "], %[g0] offset:1024\n\t"                  \
+    "global_load_lds_dwordx4 %[" #O "], %[g0] offset:2048\n\t"                  \
+    "global_load_lds_dwordx4 %[" #O "], %[g0] offset:3072\n\t"                  \
+    "s_add_u32 m0, %[l], " #LOFF4 "\n\t"                                         \
+    "s_nop 0\n\t"                                                               \
+    "global_load_lds_dwordx4 %[" #O "], %[g1]\n\t"                              \
+    "global_load_lds_dwordx4 %[" #O "], %[g1] offset:1024\n\t"
+    asm volatile("s_mov_b32 %[keep], m0\n\t"
+                 RWRT_REFILL_CORNER(o0, 0, 4096)
+                 RWRT_REFILL_CORNER(o1, 6144, 10240)
+                 RWRT_REFILL_CORNER(o2, 12288, 16384)
+                 RWRT_REFILL_CORNER(o3, 18432, 22528)
+                 "s_mov_b32 m0, %[keep]"
+                 : [keep] "=&s"(keep)
+                 : [g0] "s"(img), [g1] "s"(img_hi), [o0] "v"(o0), [o1] "v"(o1), [o2] "v"(o2),
+                   [o3] "v"(o3), [l] "s"(l)
+                 : "memory");
+#undef RWRT_REFILL_CORNER
+  }
+  // Latency mode (quad_rays): the four lanes of a quad hold one ray, and lane
+  // role r blends only records ra = r and rb = r + 4 (roles 2, 3: rb = r) of
+  // the four corners (quad_lookup_end), so each lane loads just those two
+  // chunks per corner into slots (j, 0) and (j, 1) of its slice: 8 LDS-DMA
+  // loads per refill instead of 24.  qa = ra KiB, qb = (rb - 1) KiB: slot 1
+  // is read with the instruction offset 1 KiB, which also moves the source.
+  __device__ __forceinline__ void quad_refill(unsigned o0, unsigned o1, unsigned o2, unsigned o3, unsigned qa,
+                                              unsigned qb) const {
+    typedef __attribute__((address_space(3))) char lds_char;
+    const unsigned l = (unsigned)(size_t)(lds_char*)wave_base;
+    unsigned keep;
+#define RWRT_QUAD_CORNER(O, LOFF)                                                 \
+    "v_add_u32 %[ta], %[" #O "], %[qa]\n\t"                                       \
+    "v_add_u32 %[tb], %[" #O "], %[qb]\n\t"                                       \
+    "s_add_u32 m0, %[l], " #LOFF "\n\t"                                          \
+    "s_nop 0\n\t"                                                               \
+    "global_load_lds_dwordx4 %[ta], %[g0]\n\t"                                  \
+    "global_load_lds_dwordx4 %[tb], %[g0] offset:1024\n\t"
+    unsigned ta, tb;
+    asm volatile("s_mov_b32 %[keep], m0\n\t"
+                 RWRT_QUAD_CORNER(o0, 0)
+                 RWRT_QUAD_CORNER(o1, 2048)
+                 RWRT_QUAD_CORNER(o2, 4096)
+                 RWRT_QUAD_CORNER(o3, 6144)
+                 "s_mov_b32 m0, %[keep]"
+                 : [keep] "=&s"(keep), [ta] "=&v"(ta), [tb] "=&v"(tb)
+                 : [g0] "s"(img), [o0] "v"(o0), [o1] "v"(o1), [o2] "v"(o2), [o3] "v"(o3), [qa] "v"(qa),
+                   [qb] "v"(qb), [l] "s"(l)
+                 : "memory");
+#undef RWRT_QUAD_CORNER
+  }
+  __device__ __forceinline__ Pending quad_begin(double lon, double lat, unsigned qa, unsigned qb) const {
+    const Corners k = corners(F, py_mod_2pi(lon), lat);
+    if (k.key_x != key_x || k.key_y != key_y) {
+      quad_refill(img_offset(k.pa), img_offset(k.pb), img_offset(k.pc), img_offset(k.pd), qa, qb);
+      key_x = k.key_x;
+      key_y = k.key_y;
+    }
+    return Pending{k.wa, k.wb, k.wc, k.wd};
+  }
   __device__ __forceinline__ Pending begin(double lon, double lat) const {
     const Corners k = corners(F, py_mod_2pi(lon), lat);
     const bool miss = k.key_x != key_x || k.key_y != key_y;
-    if (miss) {   // miss: refill the slice by LDS-DMA
-      const double* src[4] = {k.a, k.b, k.c, k.d};
-      char* const base = lds_slice_base(wave_base);
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int q = 0; q < 6; ++q)
-          __builtin_amdgcn_global_load_lds((global_void_ptr)(src[j] + 2 * q),
-                                           (lds_void_ptr)(base + (j * 6 + q) * 1024), 16, 0, 0);
+    if (miss) {   // miss: refill the slice by LDS-DMA from the cache image
+      refill(img_offset(k.pa), img_offset(k.pb), img_offset(k.pc), img_offset(k.pd));
       key_x = k.key_x;
       key_y = k.key_y;
     }
@@ -807,7 +908,10 @@ struct LaneBG<StaticBG> {
   static constexpr int kLdsBytes = 4 * kCacheBytesPerWave;   // 256-thread blocks
   __device__ static CachedStaticBG make(const StaticBG& B, char* lds) {
     const unsigned wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    return CachedStaticBG{B.F, lds + wave * kCacheBytesPerWave, (threadIdx.x & 63u) * 16u, ~0u, ~0u};
+    uint64_t hi = (uint64_t)(uintptr_t)(B.img + 4096);
+    asm volatile("" : "+s"(hi));   // a second base pair: chunks 4-5 address like chunks 0-3
+    return CachedStaticBG{B.F, B.img, lds + wave * kCacheBytesPerWave, (const char*)(uintptr_t)hi,
+                          (threadIdx.x & 63u) * 16u, ~0u, ~0u};
   }
 };
 template <>
@@ -1958,13 +2062,14 @@ __device__ __forceinline__ void quad_lookup_end(const CachedStaticBG& B, const Q
   k.wb = p.wb;
   k.wc = p.wc;
   k.wd = p.wd;
-  const int ra = R.role, rb = R.high ? R.role : R.role + 4;   // (roles 2, 3: a duplicate read)
+  // records ra = role and rb = role + 4 (roles 2, 3: role again) of corner j
+  // sit in this lane's slots (j, 0) and (j, 1) (CachedStaticBG::quad_refill)
   const char* base = B.wave_base + B.lane16;
   double2 va[4], vb[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    va[j] = *reinterpret_cast<const double2*>(base + (j * 6 + ra) * 1024);
-    vb[j] = *reinterpret_cast<const double2*>(base + (j * 6 + rb) * 1024);
+    va[j] = *reinterpret_cast<const double2*>(base + (j * 2) * 1024);
+    vb[j] = *reinterpret_cast<const double2*>(base + (j * 2 + 1) * 1024);
   }
   const double ax = blend(k, va[0].x, va[1].x, va[2].x, va[3].x);
   const double ay = blend(k, va[0].y, va[1].y, va[2].y, va[3].y);
@@ -1993,7 +2098,8 @@ __device__ __forceinline__ void quad_rhs(const CachedStaticBG& B, const QuadRole
   double g[11];
   const auto trig = np_math::nm_sincostan_begin(lat);
   const KapTerms kw = kap_terms(kx, ky);
-  const auto pending = lookup_begin(B, lon, lat, 0.0);
+  const int rb = R.high ? R.role : R.role + 4;
+  const auto pending = B.quad_begin(lon, lat, (unsigned)R.role * 1024u, (unsigned)(rb - 1) * 1024u);
   double s, c, tn;
   np_math::nm_sincostan_end(lat, trig, s, c, tn);
   __builtin_amdgcn_sched_barrier(0);
@@ -2322,7 +2428,11 @@ __global__ void __launch_bounds__(256, 1) rk45_run_kernel(RunArgs<BG> a) {
   constexpr int kKBytes = 5 * 5 * 256 * 8;
   __shared__ __attribute__((aligned(16))) char smem[kKBytes + LaneBG<BG>::kLdsBytes];
   if constexpr (std::is_same<BG, StaticBG>::value) {
+#ifdef RWRT_ANALYZE_QUAD
+    if (true) {   // (analysis build of the latency mode: its loop is the common path)
+#else
     if (RARE((int)blockIdx.x < a.heavy_blocks)) {   // (block-uniform) latency mode
+#endif
       __builtin_amdgcn_s_setprio(1);
       quad_rays<kTrace>(a, smem + kKBytes, reinterpret_cast<double*>(smem));
       return;
@@ -2614,6 +2724,7 @@ __device__ __forceinline__ bool rhs_bad(const double* y) {
 
 struct Rk4Args {
   Field F;
+  const char* img;    // cache image of F (the lookups' refills)
   int64_t nray;
   double dt, cut_off;
   int32_t nt, it_begin, it_end;
@@ -2630,7 +2741,7 @@ __global__ void __launch_bounds__(256, 1) rk4_run_kernel(Rk4Args a) {
   nm_stage<NM_SINCOS | NM_TAN>();
   const int64_t nrows = a.it_end - a.it_begin;
   __shared__ __attribute__((aligned(16))) char smem[LaneBG<StaticBG>::kLdsBytes];
-  const auto RB = LaneBG<StaticBG>::make(StaticBG{a.F}, smem);
+  const auto RB = LaneBG<StaticBG>::make(StaticBG{a.F, a.img}, smem);
   const double half = 0.5 * a.dt;        // 0.5 * dt      (wr.py:602-604)
   const double sixth = a.dt / 6.0;       // dt / 6.0      (wr.py:92)
   for (;;) {
@@ -2994,6 +3105,8 @@ struct rwrt_ctx {
   int blocks_static = 0, blocks_f32 = 0, blocks_f64 = 0, blocks_a32 = 0;   // persistent grids
   uint8_t* flags = nullptr;
   size_t cap = 0;
+  char* img = nullptr;         // cache image of the static state (cache_image_kernel), rebuilt per call
+  size_t img_cap = 0;
   hipStream_t side = nullptr;
   hipEvent_t flagged = nullptr, filled = nullptr;
   hipEvent_t done = nullptr;   // end of the last call on this context
@@ -3035,6 +3148,29 @@ rwrt_status ctx_flags(rwrt_ctx* c, int64_t nray) {
     return fail(RWRT_ERR_HIP, "frozen-ray flag allocation failed%s");
   c->cap = cap;
   return RWRT_OK;
+}
+
+// The cache image of F for this call, built on `stream` (after ctx_begin:
+// the previous call of the context, which may still read the old image, is
+// finished on the device by then).  Rebuilt every call, so a caller may change
+// the packed state between calls; ~1 MB at 2.5 degrees.
+rwrt_status ctx_image(rwrt_ctx* c, const Field& F, hipStream_t stream, const char** out) {
+  const size_t need = cache_image_bytes((int64_t)F.W * F.H);
+  if (need > c->img_cap) {
+    if (c->img) {
+      if ((c->used && hipEventSynchronize(c->done) != hipSuccess) || hipFree(c->img) != hipSuccess)
+        return check_launch("releasing the context's cache image");
+      c->img = nullptr;
+      c->img_cap = 0;
+    }
+    if (hipMalloc(reinterpret_cast<void**>(&c->img), need) != hipSuccess)
+      return fail(RWRT_ERR_HIP, "cache image allocation failed%s");
+    c->img_cap = need;
+  }
+  hipLaunchKernelGGL(cache_image_kernel, dim3(grid_for((int64_t)F.W * F.H * 6, 256)), dim3(256), 0, stream,
+                     F, c->img);
+  *out = c->img;
+  return check_launch("cache_image_kernel");
 }
 
 template <class BG> int& ctx_blocks(rwrt_ctx* c);
@@ -3129,6 +3265,9 @@ rwrt_status launch_run(rwrt_ctx* ctx, const BG& B, int64_t nray, const rwrt_para
                            ctx->flags);
       }))
     return s;
+  if constexpr (std::is_same<BG, StaticBG>::value) {
+    if (rwrt_status s = ctx_image(ctx, B.F, st, &a.B.img)) return s;
+  }
   // latency mode in the run kernel's first team_blocks blocks (quad_rays):
   // one grid, so they are placed beside the persistent blocks whatever the
   // hardware queues' dispatch order (a second kernel on another stream could
@@ -3358,6 +3497,7 @@ rwrt_status rwrt_ctx_destroy(rwrt_ctx* c) {
     // the last call's kernels may still read the flags / run on the side stream
     if (c->used && hipEventSynchronize(c->done) != hipSuccess) s = check_launch("rwrt_ctx_destroy");
     if (c->flags) (void)hipFree(c->flags);
+    if (c->img) (void)hipFree(c->img);
     if (c->side) (void)hipStreamDestroy(c->side);
     if (c->flagged) (void)hipEventDestroy(c->flagged);
     if (c->filled) (void)hipEventDestroy(c->filled);
@@ -3563,7 +3703,7 @@ rwrt_status rwrt_rk4_run(rwrt_ctx* ctx, const rwrt_grid* g, const double* d_pack
   hipStream_t st = (hipStream_t)stream;
   if (hipMemsetAsync(d_work, 0, sizeof(int32_t), st) != hipSuccess)
     return check_launch("hipMemsetAsync(queue)");
-  Rk4Args a{F, nray, p->tstep, p->cut_off, p->nt, it_begin, it_end, d_order, d_state, d_count,
+  Rk4Args a{F, nullptr, nray, p->tstep, p->cut_off, p->nt, it_begin, it_end, d_order, d_state, d_count,
             d_nanrow, d_out, d_work, nullptr};
   int64_t blocks = ctx_persistent_blocks<StaticBG>(ctx);
   const int64_t need = (nray + 255) / 256;
@@ -3577,6 +3717,7 @@ rwrt_status rwrt_rk4_run(rwrt_ctx* ctx, const rwrt_grid* g, const double* d_pack
                            ctx->flags);
       }))
     return s;
+  if (rwrt_status s = ctx_image(ctx, F, st, &a.img)) return s;
   hipLaunchKernelGGL(rk4_run_kernel, dim3((unsigned)blocks), dim3(256), 0, st, a);
   if (rwrt_status s = check_launch("rk4_run_kernel")) return s;
   hipLaunchKernelGGL(rk4_fill_kernel, dim3((unsigned)((nray + kFillThreads - 1) / kFillThreads)),

@@ -10,6 +10,7 @@
 #   ab:<lib>,<lib>..:<reps>[:<bench args>]   interleaved A/B bench lines of library builds
 #   prof:<tag>[:<bench args>]    same-build profile (tools/profile_round.sh <tag> <args>)
 #   py:<script and args>         python3 <script and args>
+#   sh:<command>                 any shell command (e.g. RWRT_LIB=... python3 tools/...)
 set -o pipefail
 name=$1; shift
 O=gpurun_out/$name
@@ -62,6 +63,9 @@ for step in "$@"; do
     py)
       timeout -k 10 900 python3 -u $rest > $O/py_$n.log 2>&1 || { tail -30 $O/py_$n.log; exit 1; }
       tail -5 $O/py_$n.log ;;
+    sh)
+      timeout -k 10 900 bash -c "$rest" > $O/sh_$n.log 2>&1 || { tail -30 $O/sh_$n.log; exit 1; }
+      tail -6 $O/sh_$n.log ;;
     *)
       echo "unknown step $step"; exit 2 ;;
   esac
