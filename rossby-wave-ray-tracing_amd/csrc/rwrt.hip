@@ -430,6 +430,9 @@ __device__ __forceinline__ void lds_dma_wait() { asm volatile("s_waitcnt vmcnt(0
 #ifndef RWRT_CACHE_READ_GROUPS
 #define RWRT_CACHE_READ_GROUPS 2
 #endif
+#ifndef RWRT_KAP_IN_LOOKUP   // the wavenumber terms under the cell cache's first reads: +0.3 % (r4e)
+#define RWRT_KAP_IN_LOOKUP 1
+#endif
 static_assert(RWRT_CACHE_READ_GROUPS >= 1 && 6 % RWRT_CACHE_READ_GROUPS == 0,
               "RWRT_CACHE_READ_GROUPS must divide the 6 chunks of a record (1, 2, 3 or 6)");
 
@@ -558,7 +561,10 @@ struct CachedStaticBG {
     }
     return Pending{k.wa, k.wb, k.wc, k.wd};
   }
-  __device__ __forceinline__ void end(const Pending& p, double g[11]) const {
+  // fill(): independent work placed between the first group's reads and its
+  // blends (the reads' latency; nothing else is in flight there)
+  template <class Fill>
+  __device__ __forceinline__ void end(const Pending& p, double g[11], Fill&& fill) const {
     lds_dma_wait();
     Corners k;
     k.wa = p.wa;
@@ -573,6 +579,7 @@ struct CachedStaticBG {
       for (int q = 0; q < kQ; ++q)
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j][q] = chunk(j, q0 + q);
+      if (q0 == 0) fill();
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int q = 0; q < kQ; ++q) {
@@ -596,7 +603,20 @@ __device__ __forceinline__ CachedStaticBG::Pending lookup_begin(const CachedStat
 }
 __device__ __forceinline__ void lookup_end(const CachedStaticBG& B,
                                            const CachedStaticBG::Pending& p, double g[11]) {
-  B.end(p, g);
+  B.end(p, g, [] {});
+}
+template <class Fill>
+__device__ __forceinline__ void lookup_end(const CachedStaticBG& B, const CachedStaticBG::Pending& p,
+                                           double g[11], Fill&& fill) {
+  B.end(p, g, fill);
+}
+// (the other backgrounds: the independent work first)
+template <class BG, class Fill>
+__device__ __forceinline__ void lookup_end(const BG& B, const typename std::decay<decltype(lookup_begin(
+                                                            B, 0.0, 0.0, 0.0))>::type& p,
+                                           double g[11], Fill&& fill) {
+  fill();
+  lookup_end(B, p, g);
 }
 
 template <class T>
@@ -1307,12 +1327,21 @@ __device__ __forceinline__ void ray_rhs(const BG& B, double t, const double* y, 
   const auto trig = np_math::nm_sincostan_begin(lat);
   double s, c;
   DivGuard G;
+#if RWRT_KAP_IN_LOOKUP
+  KapTermsR kw;
+#else
   const KapTermsR kw = kap_terms_r(kx, ky, G);   // (k, l only: beside the trig and the cell arithmetic)
+#endif
   const auto pending = lookup_begin(B, lon, lat, t);   // the lookup's fill overlaps the trig
   double tn;
   np_math::nm_sincostan_end(lat, trig, s, c, tn);   // == k_sincostan(lat, s, c, tn)
   __builtin_amdgcn_sched_barrier(0);
+#if RWRT_KAP_IN_LOOKUP
+  // the wavenumber terms (k, l only) under the cell cache's first reads
+  lookup_end(B, pending, g, [&] { kw = kap_terms_r(kx, ky, G); });
+#else
   lookup_end(B, pending, g);
+#endif
   const Merc M = merc_factors(lat, c, s);
   double ug, vg;
   if (RARE(!rhs_tail_fast(g, M, s, c, tn, kx, kw, G, amp, dy, ug, vg))) {

@@ -71,6 +71,7 @@ class RayEngine:
 
     bg = None   # rwrt_background of a time-varying state (None: the reference's static state)
     split_rho = None   # the last advance()'s rank correlation of its leading launches (split="auto")
+    launch_log = ()    # the last advance()'s launches: rows and latency-mode decision
     _ctx = None
 
     @property
@@ -532,6 +533,7 @@ class RayEngine:
             order = self.live_first_order_of(st)
         works = []          # per-ray attempts of the launches so far (the last two)
         self.split_rho = None
+        self.launch_log = []   # per launch: rows, rays in latency mode (diagnostics)
         k = 0
         while k < len(bounds):
             i0, i1 = bounds[k]
@@ -557,6 +559,7 @@ class RayEngine:
             # (a list: one latency-mode size per launch, the last repeated)
             tk = team[min(k, len(team) - 1)] if isinstance(team, list) else team
             n_heavy, qpw = self.team_size(tk, st, work, order, i1 - i0) if tk else (0, 16)
+            self.launch_log.append({"rows": [int(i0), int(i1)], "n_heavy": int(n_heavy), "per_wave": int(qpw)})
             if os.environ.get("RWRT_DEBUG_TEAM"):
                 print(f"launch rows [{i0}, {i1}): n_heavy {n_heavy} at {qpw} per wave", flush=True)
             prev_work = cnt.sum(1)

@@ -59,8 +59,16 @@ def main():
         for r in range(w):
             dt, res = timed(lambda: run_sharded(eng, y0, nt, rank=r, world=w, gather=False,
                                                        team=team, lead=lead))
+            ev = []
+            run_sharded(eng, y0, nt, rank=r, world=w, gather=False, team=team, lead=lead, events=ev)
+            torch.cuda.synchronize()
+            launches = [dict(d, ms=a_.elapsed_time(b_)) for d, (a_, b_) in
+                        zip([{"rows": [1, 1 + 6], "n_heavy": 0, "per_wave": 16}] + list(eng.launch_log), ev)]
+            att = (res.res.nacc + res.res.nrej)
             ranks.append({"rank": r, "s": dt, "rays": int(res.idx.numel()), "ray_steps": res.steps_local,
-                          "max_attempts": int((res.res.nacc + res.res.nrej).max().item())})
+                          "max_attempts": int(att.max().item()),
+                          "top_attempts": [int(x) for x in torch.topk(att, min(8, att.numel())).values.tolist()],
+                          "launches": launches})
         steps = sum(x["ray_steps"] for x in ranks)
         mk = max(x["s"] for x in ranks)
         out["worlds"][str(w)] = {"makespan_s": mk, "rate": steps / mk, "ray_steps": steps, "ranks": ranks}
