@@ -422,19 +422,17 @@ __device__ __forceinline__ char* lds_slice_base(char* wave_base) {
 // that carry scopes too -- which these (through lds_slice_base) do not.
 __device__ __forceinline__ void lds_dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-// The static cached lookup reads its cell's LDS slice in this many groups,
-// each group's reads in flight together before its blends.  Two groups (48
-// VGPRs in flight instead of 96) take the run kernel's VGPR spills to AGPRs
-// from 158 to 8: C3 +2.3 % zonal, +1.5 % non-zonal over one group, three
-// groups in between (profiles/r3/sched/pass_ee_cache_read_groups.txt)
-#ifndef RWRT_CACHE_READ_GROUPS
-#define RWRT_CACHE_READ_GROUPS 2
-#endif
+// The static cached lookup reads its cell's LDS slice in two groups (chunks
+// 0-2, 3-5), each group's reads in flight before its blends: 48 VGPRs of reads
+// in flight instead of 96 takes the run kernel's VGPR spills to AGPRs from 158
+// to 8 (C3 +2.3 % zonal, +1.5 % non-zonal over one group, three groups in
+// between: profiles/r3/sched/pass_ee_cache_read_groups.txt).  The refill is
+// ordered to match (CachedStaticBG::refill), so the first group waits for part
+// of it only.
+constexpr int kCacheReadGroups = 2;
 #ifndef RWRT_KAP_IN_LOOKUP   // the wavenumber terms under the cell cache's first reads: +0.3 % (r4e)
 #define RWRT_KAP_IN_LOOKUP 1
 #endif
-static_assert(RWRT_CACHE_READ_GROUPS >= 1 && 6 % RWRT_CACHE_READ_GROUPS == 0,
-              "RWRT_CACHE_READ_GROUPS must divide the 6 chunks of a record (1, 2, 3 or 6)");
 
 // The cache image of the static state: the records of 64 consecutive grid
 // points stored chunk-major, so that a corner's six 16-B chunks lie 1 KiB
@@ -488,28 +486,36 @@ struct CachedStaticBG {
     typedef __attribute__((address_space(3))) char lds_char;
     const unsigned l = (unsigned)(size_t)(lds_char*)wave_base;
     unsigned keep;
-#define RWRT_REFILL_CORNER(O, LOFF, LOFF4)                                        \
+#define RWRT_REFILL_LO(O, LOFF)                                                  \
     "s_add_u32 m0, %[l], " #LOFF "\n\t"                                          \
     "s_nop 0\n\t"                                                               \
     "global_load_lds_dwordx4 %[" #O "], %[g0]\n\t"                              \
     "global_load_lds_dwordx4 %[" #O "], %[g0] offset:1024\n\t"                  \
     "global_load_lds_dwordx4 %[" #O "], %[g0] offset:2048\n\t"                  \
-    "global_load_lds_dwordx4 %[" #O "], %[g0] offset:3072\n\t"                  \
+    "global_load_lds_dwordx4 %[" #O "], %[g0] offset:3072\n\t"
+#define RWRT_REFILL_HI(O, LOFF4)                                                 \
     "s_add_u32 m0, %[l], " #LOFF4 "\n\t"                                         \
     "s_nop 0\n\t"                                                               \
     "global_load_lds_dwordx4 %[" #O "], %[g1]\n\t"                              \
     "global_load_lds_dwordx4 %[" #O "], %[g1] offset:1024\n\t"
+    // chunks 0-3 of every corner first (16 loads), then chunks 4-5 (8): the
+    // first read group (chunks 0-2) waits for the first 16 only (vmcnt(8), end())
     asm volatile("s_mov_b32 %[keep], m0\n\t"
-                 RWRT_REFILL_CORNER(o0, 0, 4096)
-                 RWRT_REFILL_CORNER(o1, 6144, 10240)
-                 RWRT_REFILL_CORNER(o2, 12288, 16384)
-                 RWRT_REFILL_CORNER(o3, 18432, 22528)
+                 RWRT_REFILL_LO(o0, 0)
+                 RWRT_REFILL_LO(o1, 6144)
+                 RWRT_REFILL_LO(o2, 12288)
+                 RWRT_REFILL_LO(o3, 18432)
+                 RWRT_REFILL_HI(o0, 4096)
+                 RWRT_REFILL_HI(o1, 10240)
+                 RWRT_REFILL_HI(o2, 16384)
+                 RWRT_REFILL_HI(o3, 22528)
                  "s_mov_b32 m0, %[keep]"
                  : [keep] "=&s"(keep)
                  : [g0] "s"(img), [g1] "s"(img_hi), [o0] "v"(o0), [o1] "v"(o1), [o2] "v"(o2),
                    [o3] "v"(o3), [l] "s"(l)
                  : "memory");
-#undef RWRT_REFILL_CORNER
+#undef RWRT_REFILL_LO
+#undef RWRT_REFILL_HI
   }
   // Latency mode (quad_rays): the four lanes of a quad hold one ray, and lane
   // role r blends only records ra = r and rb = r + 4 (roles 2, 3: rb = r) of
@@ -565,15 +571,19 @@ struct CachedStaticBG {
   // blends (the reads' latency; nothing else is in flight there)
   template <class Fill>
   __device__ __forceinline__ void end(const Pending& p, double g[11], Fill&& fill) const {
-    lds_dma_wait();
+    // the refill's first 16 loads (chunks 0-3) have landed once at most its
+    // last 8 are outstanding: loads complete in order (the second group
+    // waits for them all)
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     Corners k;
     k.wa = p.wa;
     k.wb = p.wb;
     k.wc = p.wc;
     k.wd = p.wd;
-    constexpr int kQ = 6 / RWRT_CACHE_READ_GROUPS;
+    constexpr int kQ = 6 / kCacheReadGroups;
 #pragma unroll
     for (int q0 = 0; q0 < 6; q0 += kQ) {
+      if (q0 > 0) lds_dma_wait();   // (the rest of the refill)
       double2 v[4][kQ];   // every read of the group in flight before its first blend
 #pragma unroll
       for (int q = 0; q < kQ; ++q)
@@ -2406,12 +2416,14 @@ __device__ __forceinline__ void quad_rays(const RunArgs<StaticBG>& a, char* cach
     if (writer) {
       const double2 r0 = make_double2(y[0], y[1]), r1 = make_double2(y[2], y[3]);
       const double2 r2 = make_double2(y[4], ug), r3 = make_double2(vg, (double)nacc);
+      // non-temporal, like the run kernel's: rows stream past the L2 that
+      // holds the cache image the refills read
       for (int kr = it; kr < last; ++kr) {
         double2* o = reinterpret_cast<double2*>(a.out + ((size_t)ray * nrows + (kr - a.it_begin)) * RWRT_NOUT);
-        o[0] = r0;
-        o[1] = r1;
-        o[2] = r2;
-        o[3] = r3;
+        store_row16<1>(o + 0, r0);
+        store_row16<1>(o + 1, r1);
+        store_row16<1>(o + 2, r2);
+        store_row16<1>(o + 3, r3);
       }
     }
     if (nanrow == a.nt && isnan(y[0])) nanrow = it;   // wr.py:853-855 (host reduces)

@@ -47,7 +47,9 @@ def main():
     ap.add_argument("--team", default="auto", help="latency-mode rays per launch (int or 'auto')")
     ap.add_argument("--lead", default="24,96", help="rows of the re-ordering launches after the probe (bench.py default for N > 1)")
     a = ap.parse_args()
-    team = a.team if a.team == "auto" else int(a.team)
+    # 'auto', an int (rays per launch at 16 per wave) or n:q (n rays at q per wave)
+    team = a.team if a.team == "auto" else (tuple(int(x) for x in a.team.split(":")) if ":" in a.team
+                                             else int(a.team))
     lead = [int(x) for x in a.lead.split(",") if x]
     bs, bg = bench.make_bs(a.bg)
     y0 = torch.as_tensor(bench.c3_initial_state(bs), device="cuda")
