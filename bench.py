@@ -227,19 +227,22 @@ def schedule_defaults(args, world):
       probe           4 rows for a whole C3 set (+0.75 % over 6 with the
                       per-launch latency mode, profiles/r3/sched/pass_w_*),
                       6 otherwise;
-      latency mode    a whole zonal C3 set: 64 / 256 / 64 heaviest rays in the
-                      24- / 160- / rest launches (the 160-row launch is bound
-                      by its heaviest rays' chains; +0.9 %, pass_u_*); a whole
-                      non-zonal set: none (its chain-bound rays are not the
-                      predicted heaviest; 64/256/64 costs 1.5 %, pass_x_*); a
-                      split set: the auto rule (RayEngine.team_size)."""
+      latency mode    a whole zonal C3 set: the 64 heaviest rays of each
+                      launch after the probe (one latency-mode block: the
+                      launches are bound by their heaviest rays' chains; 64 /
+                      64 / 64 measured +0.4 % over round 3's 64 / 256 / 64 and
+                      +1.3 % over none, profiles/r4/sched/team.txt -- more
+                      latency-mode blocks make each attempt slower, DESIGN.md
+                      §4); a whole non-zonal set: none (its chain-bound rays
+                      are not the predicted heaviest; 64/256/64 costs 1.5 %,
+                      pass_x_*); a split set: the auto rule (RayEngine.team_size)."""
     whole = args.config == "C3" and (world == 1 or args.scaling == "weak")
     if args.first_chunk is None:
         args.first_chunk = "24,160" if whole else "24,96"
     if args.probe is None:
         args.probe = 4 if whole else 6
     if args.team is None:
-        args.team = ("64,256,64" if args.bg == "zonal" else "0") if whole else "auto"
+        args.team = ("64,64,64" if args.bg == "zonal" else "0") if whole else "auto"
     return args
 
 
@@ -355,7 +358,7 @@ def main():
     ap.add_argument("--team", default=None,
                     help="rays per launch in latency mode (quad_rays: four lanes of a wave per ray); "
                          "an integer, one per launch after the probe (e.g. 64,256,64; the last "
-                         "repeats) or 'auto' (RayEngine.team_size).  Default: 64,256,64 for a whole C3 "
+                         "repeats) or 'auto' (RayEngine.team_size).  Default: 64,64,64 for a whole C3 "
                          "set per GPU, auto for a split one")
     ap.add_argument("--lib", default=None, help="alternative librwrt build (A/B timing)")
     ap.add_argument("--traffic", default=None, help="traffic.json (tools/pmc_traffic.py)")

@@ -104,13 +104,13 @@ def test_schedule_defaults():
         base.update(kw)
         return argparse.Namespace(**base)
     a = bench.schedule_defaults(ns(), 1)
-    assert (a.first_chunk, a.probe, a.team) == ("24,160", 4, "64,256,64")
+    assert (a.first_chunk, a.probe, a.team) == ("24,160", 4, "64,64,64")
     a = bench.schedule_defaults(ns(bg="nonzonal"), 8)
     assert (a.first_chunk, a.probe, a.team) == ("24,160", 4, "0")
     a = bench.schedule_defaults(ns(scaling="strong"), 8)
     assert (a.first_chunk, a.probe, a.team) == ("24,96", 6, "auto")
     a = bench.schedule_defaults(ns(scaling="strong"), 1)
-    assert (a.first_chunk, a.probe, a.team) == ("24,160", 4, "64,256,64")
+    assert (a.first_chunk, a.probe, a.team) == ("24,160", 4, "64,64,64")
     a = bench.schedule_defaults(ns(config="C5"), 1)
     assert (a.first_chunk, a.probe, a.team) == ("24,96", 6, "auto")
     a = bench.schedule_defaults(ns(probe=6, team="0", first_chunk="24"), 1)

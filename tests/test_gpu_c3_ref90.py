@@ -87,10 +87,10 @@ def check(g, hist, counts):
 def test_c3_90d_sample_bitwise_with_reference_arithmetic(kind):
     """The bench's own schedule for a whole set (bench.schedule_defaults: a
     4-row probe, 24 + 160 rows, the adaptive split of the long launch; latency
-    mode 64 / 256 / 64 on the zonal jets, none on the non-zonal set, where the
+    mode 64 / 64 / 64 on the zonal jets, none on the non-zonal set, where the
     split must actually happen)."""
     info = {}
-    g, hist, counts = run_c3_90d(kind, team=[64, 256, 64] if kind == "zonal" else 0, probe=4, split="auto",
+    g, hist, counts = run_c3_90d(kind, team=[64, 64, 64] if kind == "zonal" else 0, probe=4, split="auto",
                                  info=info)
     check(g, hist, counts)
     if kind == "nonzonal":
