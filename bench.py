@@ -218,6 +218,16 @@ def roofline(steps_per_launch, avg_launch_s, workload, schedule, bytes_per_step,
     return out
 
 
+def _split_arg(s):
+    """--split: 'off', 'auto' or 'auto:a,b,..' (positive row counts)"""
+    import argparse
+    head, colon, rows = s.partition(":")
+    if s in ("off", "auto") or (head == "auto" and colon and all(x.isdigit() and int(x) > 0
+                                                                  for x in rows.split(","))):
+        return s
+    raise argparse.ArgumentTypeError(f"--split: 'off', 'auto' or 'auto:a,b,..', not {s!r}")
+
+
 def schedule_defaults(args, world):
     """The schedule knobs left unset on the command line, by what one GPU
     holds: a whole C3 set (one GPU, or weak scaling) or a split one / C5.
@@ -352,9 +362,10 @@ def main():
                          "levels and an fp32 RHS (fp64 positions, time and stepper)")
     ap.add_argument("--c5-periods", type=int, default=5,
                     help="C5 periods (1-5 of the C3 list; 5 = 9.67 M slots, ~4 M live rays: BASELINE's size)")
-    ap.add_argument("--split", default="auto", choices=["auto", "off"],
-                    help="split the long launch once more when the leading launches' per-ray work "
-                         "predicts the next poorly (RayEngine.SPLIT_RHO)")
+    ap.add_argument("--split", default="auto", type=_split_arg,
+                    help="'auto': split the long launch once more when the leading launches' per-ray "
+                         "work predicts the next poorly (RayEngine.SPLIT_RHO), after SPLIT_ROWS rows; "
+                         "'auto:a,b,..': cut after a, a+b, .. rows instead; 'off'")
     ap.add_argument("--team", default=None,
                     help="rays per launch in latency mode (quad_rays: four lanes of a wave per ray); "
                          "an integer, one per launch after the probe (e.g. 64,256,64; the last "

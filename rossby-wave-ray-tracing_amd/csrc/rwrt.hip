@@ -422,14 +422,17 @@ __device__ __forceinline__ char* lds_slice_base(char* wave_base) {
 // that carry scopes too -- which these (through lds_slice_base) do not.
 __device__ __forceinline__ void lds_dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-// The static cached lookup reads its cell's LDS slice in two groups (chunks
-// 0-2, 3-5), each group's reads in flight before its blends: 48 VGPRs of reads
-// in flight instead of 96 takes the run kernel's VGPR spills to AGPRs from 158
-// to 8 (C3 +2.3 % zonal, +1.5 % non-zonal over one group, three groups in
-// between: profiles/r3/sched/pass_ee_cache_read_groups.txt).  The refill is
-// ordered to match (CachedStaticBG::refill), so the first group waits for part
-// of it only.
-constexpr int kCacheReadGroups = 2;
+// The static cached lookup reads its cell's LDS slice software-pipelined by
+// chunk (4 reads, 16 VGPRs each): chunk q is blended while chunk q + 1 is in
+// flight, and chunk q + 2 is issued once q's registers are free.  All 24
+// reads in flight at once (96 VGPRs) spilled 158 VGPRs to AGPRs; round 3's
+// two groups of 12 (48 VGPRs) removed the spills (+2.3 %,
+// profiles/r3/sched/pass_ee_cache_read_groups.txt) but left the second
+// group's latency exposed; one chunk ahead: +1.5 % over the two groups, two
+// chunks ahead +0.0 % (profiles/r4/sched/cache_pipe.txt).  The refill is
+// ordered to match (CachedStaticBG::refill): chunks 0-3 of every corner
+// first, so the first reads wait for part of it only.
+constexpr int kCacheAhead = 1;
 #ifndef RWRT_KAP_IN_LOOKUP   // the wavenumber terms under the cell cache's first reads: +0.3 % (r4e)
 #define RWRT_KAP_IN_LOOKUP 1
 #endif
@@ -499,7 +502,7 @@ struct CachedStaticBG {
     "global_load_lds_dwordx4 %[" #O "], %[g1]\n\t"                              \
     "global_load_lds_dwordx4 %[" #O "], %[g1] offset:1024\n\t"
     // chunks 0-3 of every corner first (16 loads), then chunks 4-5 (8): the
-    // first read group (chunks 0-2) waits for the first 16 only (vmcnt(8), end())
+    // reads of chunks 0-3 wait for the first 16 only (vmcnt(8), end())
     asm volatile("s_mov_b32 %[keep], m0\n\t"
                  RWRT_REFILL_LO(o0, 0)
                  RWRT_REFILL_LO(o1, 6144)
@@ -567,36 +570,40 @@ struct CachedStaticBG {
     }
     return Pending{k.wa, k.wb, k.wc, k.wd};
   }
-  // fill(): independent work placed between the first group's reads and its
-  // blends (the reads' latency; nothing else is in flight there)
+  // fill(): independent work placed between the first reads and the first
+  // blend (the reads' latency; nothing else is in flight there)
   template <class Fill>
   __device__ __forceinline__ void end(const Pending& p, double g[11], Fill&& fill) const {
     // the refill's first 16 loads (chunks 0-3) have landed once at most its
-    // last 8 are outstanding: loads complete in order (the second group
-    // waits for them all)
+    // last 8 are outstanding: loads complete in order (chunk 4's reads wait
+    // for them all)
     asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     Corners k;
     k.wa = p.wa;
     k.wb = p.wb;
     k.wc = p.wc;
     k.wd = p.wd;
-    constexpr int kQ = 6 / kCacheReadGroups;
+    constexpr int kAhead = kCacheAhead;
+    double2 v[6][4];
 #pragma unroll
-    for (int q0 = 0; q0 < 6; q0 += kQ) {
-      if (q0 > 0) lds_dma_wait();   // (the rest of the refill)
-      double2 v[4][kQ];   // every read of the group in flight before its first blend
+    for (int q = 0; q <= kAhead; ++q)
 #pragma unroll
-      for (int q = 0; q < kQ; ++q)
+      for (int j = 0; j < 4; ++j) v[q][j] = chunk(j, q);
+    fill();
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j][q] = chunk(j, q0 + q);
-      if (q0 == 0) fill();
+    for (int q = 0; q < 6; ++q) {
+      const int f = 2 * q;
+      g[f] = blend(k, v[q][0].x, v[q][1].x, v[q][2].x, v[q][3].x);
+      if (f + 1 < 11) g[f + 1] = blend(k, v[q][0].y, v[q][1].y, v[q][2].y, v[q][3].y);
       __builtin_amdgcn_sched_barrier(0);
+      const int n = q + kAhead + 1;
+      if (n < 6) {
+        if (n == 4) lds_dma_wait();
 #pragma unroll
-      for (int q = 0; q < kQ; ++q) {
-        const int f = 2 * (q0 + q);
-        g[f] = blend(k, v[0][q].x, v[1][q].x, v[2][q].x, v[3][q].x);
-        if (f + 1 < 11) g[f + 1] = blend(k, v[0][q].y, v[1][q].y, v[2][q].y, v[3][q].y);
+        for (int j = 0; j < 4; ++j) v[n][j] = chunk(j, n);
       }
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
   // Only the RHS looks up through the cache: a lane with |lat| > pi/2 is

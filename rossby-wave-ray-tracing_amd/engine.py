@@ -533,18 +533,27 @@ class RayEngine:
             order = self.live_first_order_of(st)
         works = []          # per-ray attempts of the launches so far (the last two)
         self.split_rho = None
+        # "auto" (one cut after SPLIT_ROWS rows) or "auto:a,b,..": cuts after a, a+b, .. rows
+        auto_split = isinstance(split, str) and split.split(":")[0] == "auto"
+        split_rows = ([int(x) for x in split.split(":", 1)[1].split(",")] if auto_split and ":" in split
+                      else [self.SPLIT_ROWS])
         self.launch_log = []   # per launch: rows, rays in latency mode (diagnostics)
         k = 0
         while k < len(bounds):
             i0, i1 = bounds[k]
-            if (split == "auto" and k == n_lead and len(works) == 2 and i1 - i0 > 2 * self.SPLIT_ROWS
+            if (auto_split and k == n_lead and len(works) == 2 and i1 - i0 > 2 * split_rows[0]
                     and order_policy in ("cost", "priority", "total")):
                 live = ~torch.isnan(st["state"][:5].sum(0))
                 rho = self.rank_corr(works[0], works[1], live)
                 self.split_rho = rho
                 if rho < self.SPLIT_RHO:
-                    bounds[k:k + 1] = [(i0, i0 + self.SPLIT_ROWS), (i0 + self.SPLIT_ROWS, i1)]
-                    i1 = i0 + self.SPLIT_ROWS
+                    cuts = [i0]
+                    for n in split_rows:
+                        if cuts[-1] + n < i1:
+                            cuts.append(cuts[-1] + n)
+                    cuts.append(i1)
+                    bounds[k:k + 1] = list(zip(cuts[:-1], cuts[1:]))
+                    i1 = cuts[1]
                     order_policy = "total"
                 if os.environ.get("RWRT_DEBUG_SCHED"):
                     print(f"split: rank correlation {rho:.3f} -> {'split' if rho < self.SPLIT_RHO else 'one launch'}",
@@ -570,7 +579,7 @@ class RayEngine:
                 events.append((e0, e1))
             else:
                 self.run(st, p, tb, i0, i1, view, order, n_heavy, qpw)
-            if split == "auto" and k < n_lead:
+            if auto_split and k < n_lead:
                 works = (works + [cnt.sum(1) - prev_work])[-2:]
             if sink is not None:
                 sink(i0, i1, view)

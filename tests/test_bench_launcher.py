@@ -115,3 +115,15 @@ def test_schedule_defaults():
     assert (a.first_chunk, a.probe, a.team) == ("24,96", 6, "auto")
     a = bench.schedule_defaults(ns(probe=6, team="0", first_chunk="24"), 1)
     assert (a.first_chunk, a.probe, a.team) == ("24", 6, "0")
+
+
+def test_split_argument():
+    """--split: 'off', 'auto' (one cut after RayEngine.SPLIT_ROWS) or 'auto:a,b,..'
+    (cuts after a, a+b, .. rows; profiles/r4/sched/nonzonal_split.txt)."""
+    import argparse
+    from bench import _split_arg
+    for ok in ("off", "auto", "auto:300", "auto:300,300"):
+        assert _split_arg(ok) == ok
+    for bad in ("on", "auto:", "auto:0", "auto:300,x", "auto:-5", "off:3"):
+        with pytest.raises(argparse.ArgumentTypeError):
+            _split_arg(bad)
