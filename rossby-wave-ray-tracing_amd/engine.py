@@ -533,10 +533,15 @@ class RayEngine:
             order = self.live_first_order_of(st)
         works = []          # per-ray attempts of the launches so far (the last two)
         self.split_rho = None
-        # "auto" (one cut after SPLIT_ROWS rows) or "auto:a,b,..": cuts after a, a+b, .. rows
+        # "auto" (one cut after SPLIT_ROWS rows) or "auto:a,b,..": cuts after a, a+b, .. rows;
+        # the first piece is ordered by all the work so far, later ones by the work so far
+        # too or, with a "~prev" suffix, by the previous piece's work
         auto_split = isinstance(split, str) and split.split(":")[0] == "auto"
-        split_rows = ([int(x) for x in split.split(":", 1)[1].split(",")] if auto_split and ":" in split
-                      else [self.SPLIT_ROWS])
+        spec = split.split(":", 1)[1] if auto_split and ":" in split else ""
+        later_policy = "priority" if spec.endswith("~prev") else "total"
+        spec = spec[:-len("~prev")] if spec.endswith("~prev") else spec
+        split_rows = [int(x) for x in spec.split(",")] if spec else [self.SPLIT_ROWS]
+        cut_at = None          # launch index of the first piece after a cut
         self.launch_log = []   # per launch: rows, rays in latency mode (diagnostics)
         k = 0
         while k < len(bounds):
@@ -555,9 +560,12 @@ class RayEngine:
                     bounds[k:k + 1] = list(zip(cuts[:-1], cuts[1:]))
                     i1 = cuts[1]
                     order_policy = "total"
+                    cut_at = k
                 if os.environ.get("RWRT_DEBUG_SCHED"):
                     print(f"split: rank correlation {rho:.3f} -> {'split' if rho < self.SPLIT_RHO else 'one launch'}",
                           flush=True)
+            if cut_at is not None and k == cut_at + 1:
+                order_policy = later_policy
             flat = bufs[k % len(bufs)].view(-1)
             view = flat[: nray * (i1 - i0) * H.NOUT].view(nray, i1 - i0, H.NOUT)
             work = None

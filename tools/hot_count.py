@@ -47,7 +47,7 @@ def blocks(lines):
     bl, cur = [], ["entry", []]
     for l in lines:
         s = l.strip()
-        if (s.endswith(":") and s.startswith(".LBB")) or s.startswith("; %bb."):
+        if (s.startswith(".LBB") and s.split(";")[0].strip().endswith(":")) or s.startswith("; %bb."):
             bl.append(cur)
             cur = [s.split(":")[0].replace("; ", ""), []]
             continue
