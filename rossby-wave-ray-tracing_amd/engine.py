@@ -479,6 +479,29 @@ class RayEngine:
     SPLIT_RHO = 0.7
     SPLIT_ROWS = 300
 
+    @classmethod
+    def parse_split(cls, split):
+        """``split`` -> (auto?, cut lengths in rows, order policy of the pieces
+        after the first): "auto" (one cut after SPLIT_ROWS), "auto:a,b,.." (cuts
+        after a, a+b, ..), a "~prev" suffix (later pieces ordered by the previous
+        piece's work instead of all the work so far), anything else: no cut."""
+        auto = isinstance(split, str) and split.split(":")[0] == "auto"
+        spec = split.split(":", 1)[1] if auto and ":" in split else ""
+        later = "priority" if spec.endswith("~prev") else "total"
+        spec = spec[:-len("~prev")] if spec.endswith("~prev") else spec
+        return auto, ([int(x) for x in spec.split(",")] if spec else [cls.SPLIT_ROWS]), later
+
+    @staticmethod
+    def cut_bounds(i0, i1, rows):
+        """Rows [i0, i1) cut after rows[0], rows[0] + rows[1], .. (cuts at or past
+        i1 dropped): the launches that replace one long launch."""
+        cuts = [i0]
+        for n in rows:
+            if cuts[-1] + n < i1:
+                cuts.append(cuts[-1] + n)
+        cuts.append(i1)
+        return list(zip(cuts[:-1], cuts[1:]))
+
     @staticmethod
     def rank_corr(a, b, mask):
         """Spearman rank correlation of ``a`` and ``b`` over ``mask`` (device)."""
@@ -536,11 +559,7 @@ class RayEngine:
         # "auto" (one cut after SPLIT_ROWS rows) or "auto:a,b,..": cuts after a, a+b, .. rows;
         # the first piece is ordered by all the work so far, later ones by the work so far
         # too or, with a "~prev" suffix, by the previous piece's work
-        auto_split = isinstance(split, str) and split.split(":")[0] == "auto"
-        spec = split.split(":", 1)[1] if auto_split and ":" in split else ""
-        later_policy = "priority" if spec.endswith("~prev") else "total"
-        spec = spec[:-len("~prev")] if spec.endswith("~prev") else spec
-        split_rows = [int(x) for x in spec.split(",")] if spec else [self.SPLIT_ROWS]
+        auto_split, split_rows, later_policy = self.parse_split(split)
         cut_at = None          # launch index of the first piece after a cut
         self.launch_log = []   # per launch: rows, rays in latency mode (diagnostics)
         k = 0
@@ -552,13 +571,8 @@ class RayEngine:
                 rho = self.rank_corr(works[0], works[1], live)
                 self.split_rho = rho
                 if rho < self.SPLIT_RHO:
-                    cuts = [i0]
-                    for n in split_rows:
-                        if cuts[-1] + n < i1:
-                            cuts.append(cuts[-1] + n)
-                    cuts.append(i1)
-                    bounds[k:k + 1] = list(zip(cuts[:-1], cuts[1:]))
-                    i1 = cuts[1]
+                    bounds[k:k + 1] = self.cut_bounds(i0, i1, split_rows)
+                    i1 = bounds[k][1]
                     order_policy = "total"
                     cut_at = k
                 if os.environ.get("RWRT_DEBUG_SCHED"):
