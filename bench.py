@@ -219,11 +219,9 @@ def roofline(steps_per_launch, avg_launch_s, workload, schedule, bytes_per_step,
 
 
 def _split_arg(s):
-    """--split: 'off', 'auto' or 'auto:a,b,..' (positive row counts), optionally
-    with '~prev' (pieces after the first ordered by the previous piece's work)"""
+    """--split: 'off', 'auto' or 'auto:a,b,..' (positive row counts)"""
     import argparse
     head, colon, rows = s.partition(":")
-    rows = rows[:-len("~prev")] if rows.endswith("~prev") else rows
     if s in ("off", "auto") or (head == "auto" and colon and all(x.isdigit() and int(x) > 0
                                                                   for x in rows.split(","))):
         return s
@@ -367,8 +365,7 @@ def main():
     ap.add_argument("--split", default="auto", type=_split_arg,
                     help="'auto': split the long launch once more when the leading launches' per-ray "
                          "work predicts the next poorly (RayEngine.SPLIT_RHO), after SPLIT_ROWS rows; "
-                         "'auto:a,b,..': cut after a, a+b, .. rows instead ('~prev' appended: pieces after "
-                         "the first ordered by the previous piece's work, not all so far); 'off'")
+                         "'auto:a,b,..': cut after a, a+b, .. rows instead; 'off'")
     ap.add_argument("--team", default=None,
                     help="rays per launch in latency mode (quad_rays: four lanes of a wave per ray); "
                          "an integer, one per launch after the probe (e.g. 64,256,64; the last "

@@ -481,15 +481,13 @@ class RayEngine:
 
     @classmethod
     def parse_split(cls, split):
-        """``split`` -> (auto?, cut lengths in rows, order policy of the pieces
-        after the first): "auto" (one cut after SPLIT_ROWS), "auto:a,b,.." (cuts
-        after a, a+b, ..), a "~prev" suffix (later pieces ordered by the previous
-        piece's work instead of all the work so far), anything else: no cut."""
+        """``split`` -> (auto?, cut lengths in rows): "auto" (one cut after
+        SPLIT_ROWS), "auto:a,b,.." (cuts after a, a+b, ..; an A/B knob,
+        profiles/r4/sched/nonzonal_split.txt), anything else: no cut.  Every
+        piece is ordered by all the work so far."""
         auto = isinstance(split, str) and split.split(":")[0] == "auto"
         spec = split.split(":", 1)[1] if auto and ":" in split else ""
-        later = "priority" if spec.endswith("~prev") else "total"
-        spec = spec[:-len("~prev")] if spec.endswith("~prev") else spec
-        return auto, ([int(x) for x in spec.split(",")] if spec else [cls.SPLIT_ROWS]), later
+        return auto, ([int(x) for x in spec.split(",")] if spec else [cls.SPLIT_ROWS])
 
     @staticmethod
     def cut_bounds(i0, i1, rows):
@@ -556,11 +554,7 @@ class RayEngine:
             order = self.live_first_order_of(st)
         works = []          # per-ray attempts of the launches so far (the last two)
         self.split_rho = None
-        # "auto" (one cut after SPLIT_ROWS rows) or "auto:a,b,..": cuts after a, a+b, .. rows;
-        # the first piece is ordered by all the work so far, later ones by the work so far
-        # too or, with a "~prev" suffix, by the previous piece's work
-        auto_split, split_rows, later_policy = self.parse_split(split)
-        cut_at = None          # launch index of the first piece after a cut
+        auto_split, split_rows = self.parse_split(split)   # (cuts of the long launch)
         self.launch_log = []   # per launch: rows, rays in latency mode (diagnostics)
         k = 0
         while k < len(bounds):
@@ -574,12 +568,9 @@ class RayEngine:
                     bounds[k:k + 1] = self.cut_bounds(i0, i1, split_rows)
                     i1 = bounds[k][1]
                     order_policy = "total"
-                    cut_at = k
                 if os.environ.get("RWRT_DEBUG_SCHED"):
                     print(f"split: rank correlation {rho:.3f} -> {'split' if rho < self.SPLIT_RHO else 'one launch'}",
                           flush=True)
-            if cut_at is not None and k == cut_at + 1:
-                order_policy = later_policy
             flat = bufs[k % len(bufs)].view(-1)
             view = flat[: nray * (i1 - i0) * H.NOUT].view(nray, i1 - i0, H.NOUT)
             work = None

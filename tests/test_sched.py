@@ -54,12 +54,11 @@ def test_cost_cell_order_classes_then_cells():
 
 
 def test_long_launch_cuts():
-    """split='auto[:a,b,..][~prev]' (RayEngine.parse_split / cut_bounds): the
+    """split='auto[:a,b,..]' (RayEngine.parse_split / cut_bounds): the
     pieces that replace the long launch after the leading ones."""
     from engine import RayEngine as E
-    assert E.parse_split("auto") == (True, [E.SPLIT_ROWS], "total")
-    assert E.parse_split("auto:300,300") == (True, [300, 300], "total")
-    assert E.parse_split("auto:40~prev") == (True, [40], "priority")
+    assert E.parse_split("auto") == (True, [E.SPLIT_ROWS])
+    assert E.parse_split("auto:300,300") == (True, [300, 300])
     assert E.parse_split(None)[0] is False and E.parse_split("off")[0] is False
     assert E.cut_bounds(189, 1081, [300]) == [(189, 489), (489, 1081)]
     assert E.cut_bounds(189, 1081, [300, 300]) == [(189, 489), (489, 789), (789, 1081)]
