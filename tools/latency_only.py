@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--density", type=int, default=16)
     ap.add_argument("--days", type=float, default=90)
     ap.add_argument("--run-kernel", action="store_true", help="the same rays through the run kernel instead")
+    ap.add_argument("--clone", action="store_true", help="K copies of the heaviest ray instead of the K heaviest")
+    ap.add_argument("--reps", type=int, default=1)
     a = ap.parse_args()
     bs, _ = bench.make_bs("zonal")
     y0 = torch.as_tensor(bench.c3_initial_state(bs), device="cuda")
@@ -38,16 +40,20 @@ def main():
         np.save(a.find, order[:8192].cpu().numpy())
         return
     idx = torch.as_tensor(np.load(a.load)[: a.k], device="cuda")
+    if a.clone:
+        idx = idx[:1].repeat(a.k)
     yk = y0[:, idx].contiguous()
     out = torch.empty((a.k, nt - 1, 8), dtype=torch.float64, device="cuda")
     team = 0 if a.run_kernel else (a.k, a.density)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    r = eng.integrate(yk, nt, 7200.0, ttotal=(nt - 1) * 7200.0, chunk=nt - 1, out=out, team=team)
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    att = int((r.nacc + r.nrej).max().item())
-    print(f"k {a.k} density {a.density} run_kernel {a.run_kernel}: {dt:.4f} s, {1e6 * dt / att:.2f} us/attempt")
+    for _ in range(a.reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        r = eng.integrate(yk, nt, 7200.0, ttotal=(nt - 1) * 7200.0, chunk=nt - 1, out=out, team=team)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        att = int((r.nacc + r.nrej).max().item())
+        print(f"k {a.k} density {a.density} run_kernel {a.run_kernel} clone {a.clone}: {dt:.4f} s, "
+              f"{1e6 * dt / att:.2f} us/attempt", flush=True)
 
 
 if __name__ == "__main__":
