@@ -433,9 +433,6 @@ __device__ __forceinline__ void lds_dma_wait() { asm volatile("s_waitcnt vmcnt(0
 // ordered to match (CachedStaticBG::refill): chunks 0-3 of every corner
 // first, so the first reads wait for part of it only.
 constexpr int kCacheAhead = 1;
-#ifndef RWRT_COND_WAIT   // LDS-DMA waits only when the wave refilled (A/B)
-#define RWRT_COND_WAIT 0
-#endif
 #ifndef RWRT_KAP_IN_LOOKUP   // the wavenumber terms under the cell cache's first reads: +0.3 % (r4e)
 #define RWRT_KAP_IN_LOOKUP 1
 #endif
@@ -476,12 +473,7 @@ struct CachedStaticBG {
 
   struct Pending {
     double wa, wb, wc, wd;
-    bool dma;   // some lane of the wave refilled (wave-uniform): end() must wait for it
   };
-  // The LDS-DMA waits are s_waitcnt vmcnt, which on gfx950 also counts the
-  // vector STORES still in flight (the output rows): waiting only when the wave
-  // refilled keeps an evaluation without refills off the row stores' latency
-  __device__ __forceinline__ static bool wave_any(bool c) { return __builtin_amdgcn_ballot_w64(c) != 0; }
   __device__ __forceinline__ const double2& chunk(int j, int q) const {
     return *reinterpret_cast<const double2*>(wave_base + (j * 6 + q) * 1024 + lane16);
   }
@@ -561,13 +553,12 @@ struct CachedStaticBG {
   }
   __device__ __forceinline__ Pending quad_begin(double lon, double lat, unsigned qa, unsigned qb) const {
     const Corners k = corners(F, py_mod_2pi(lon), lat);
-    const bool miss = k.key_x != key_x || k.key_y != key_y;
-    if (miss) {
+    if (k.key_x != key_x || k.key_y != key_y) {
       quad_refill(img_offset(k.pa), img_offset(k.pb), img_offset(k.pc), img_offset(k.pd), qa, qb);
       key_x = k.key_x;
       key_y = k.key_y;
     }
-    return Pending{k.wa, k.wb, k.wc, k.wd, !RWRT_COND_WAIT || wave_any(miss)};
+    return Pending{k.wa, k.wb, k.wc, k.wd};
   }
   __device__ __forceinline__ Pending begin(double lon, double lat) const {
     const Corners k = corners(F, py_mod_2pi(lon), lat);
@@ -577,7 +568,7 @@ struct CachedStaticBG {
       key_x = k.key_x;
       key_y = k.key_y;
     }
-    return Pending{k.wa, k.wb, k.wc, k.wd, !RWRT_COND_WAIT || wave_any(miss)};
+    return Pending{k.wa, k.wb, k.wc, k.wd};
   }
   // fill(): independent work placed between the first reads and the first
   // blend (the reads' latency; nothing else is in flight there)
@@ -586,7 +577,7 @@ struct CachedStaticBG {
     // the refill's first 16 loads (chunks 0-3) have landed once at most its
     // last 8 are outstanding: loads complete in order (chunk 4's reads wait
     // for them all)
-    if (p.dma) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     Corners k;
     k.wa = p.wa;
     k.wb = p.wb;
@@ -608,7 +599,7 @@ struct CachedStaticBG {
       __builtin_amdgcn_sched_barrier(0);
       const int n = q + kAhead + 1;
       if (n < 6) {
-        if (n == 4 && p.dma) lds_dma_wait();
+        if (n == 4) lds_dma_wait();
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[n][j] = chunk(j, n);
       }
@@ -2111,7 +2102,7 @@ struct QuadRole {
 // field is the same blend of the same corner values (bit for bit).
 __device__ __forceinline__ void quad_lookup_end(const CachedStaticBG& B, const QuadRole& R,
                                                 const CachedStaticBG::Pending& p, double g[11]) {
-  if (p.dma) lds_dma_wait();
+  lds_dma_wait();
   Corners k;
   k.wa = p.wa;
   k.wb = p.wb;
@@ -2476,9 +2467,6 @@ __device__ __forceinline__ void quad_rays(const RunArgs<StaticBG>& a, char* cach
 using KStore = KShared<5>;
 // kTrace: the diagnostic instantiation (rwrt_ctx_set_trace) -- the product
 // kernel carries none of the trace hooks
-#ifndef RWRT_LAT_XCD_PACK
-#define RWRT_LAT_XCD_PACK 0
-#endif
 template <class BG, bool kTrace = false>
 __global__ void __launch_bounds__(256, 1) rk45_run_kernel(RunArgs<BG> a) {
   nm_stage<NM_ALL>();
@@ -2488,13 +2476,7 @@ __global__ void __launch_bounds__(256, 1) rk45_run_kernel(RunArgs<BG> a) {
   constexpr int kKBytes = 5 * 5 * 256 * 8;
   __shared__ __attribute__((aligned(16))) char smem[kKBytes + LaneBG<BG>::kLdsBytes];
   if constexpr (std::is_same<BG, StaticBG>::value) {
-#if RWRT_LAT_XCD_PACK
-    // (A/B) latency blocks on one XCD: grid blocks 0, 8, 16, .. (blocks are
-    // dealt to the 8 XCDs round-robin)
-    const int lb = (blockIdx.x % 8 == 0) ? (int)blockIdx.x / 8 : 0x7fffffff;
-#else
-    const int lb = (int)blockIdx.x;
-#endif
+    const int lb = (int)blockIdx.x;   // (latency block index)
 #ifdef RWRT_ANALYZE_QUAD
     if (true) {   // (analysis build of the latency mode: its loop is the common path)
 #else
@@ -3346,10 +3328,7 @@ rwrt_status launch_run(rwrt_ctx* ctx, const BG& B, int64_t nray, const rwrt_para
     a.trace_cap = ctx->trace ? ctx->trace_cap : 0;
   }
   if (nray > n_heavy || team_blocks) {
-    int64_t grid = team_blocks + (nray > n_heavy ? blocks : 0);
-#if RWRT_LAT_XCD_PACK
-    if (team_blocks) grid = std::max<int64_t>(grid, 8 * (team_blocks - 1) + 1);   // (A/B: blocks 0, 8, ..)
-#endif
+    const int64_t grid = team_blocks + (nray > n_heavy ? blocks : 0);
     if (a.trace) {
       if constexpr (std::is_same<BG, StaticBG>::value)
         hipLaunchKernelGGL((rk45_run_kernel<BG, true>), dim3((unsigned)grid), dim3(256), 0, st, a);
