@@ -2326,11 +2326,15 @@ __device__ __forceinline__ void quad_rays(const RunArgs<StaticBG>& a, char* cach
   R.high = (R.role & 2) != 0;
   KQuad K{Kq + threadIdx.x};
   const int64_t nrows = a.it_end - a.it_begin;
-  // order position of this quad's ray: the heaviest rays one per wave first
-  // (position p -> wave p % waves, quad p / waves), a.quad_per_wave quads per wave
+  // order position of this quad's ray, a.quad_per_wave quads per wave
   const int qi = (threadIdx.x & 63) >> 2;
-  const int64_t waves = 4 * (int64_t)a.heavy_blocks;
-  const int64_t w = qi * waves + lb * 4 + (threadIdx.x >> 6);
+  // consecutive positions share a wave (p -> wave p / quad_per_wave): rays of
+  // like weight, which on C3 are often near-copies whose row ends and cell
+  // crossings stay aligned.  Dealing the heaviest one per wave instead (p ->
+  // wave p % waves) mixed rays that diverge: the 256 heaviest C3 rays at 4 per
+  // wave took 14.5 us per attempt of the heaviest, 9.6 us contiguous
+  // (profiles/r4/sched/latency_xcd.txt)
+  const int64_t w = (lb * 4 + (int64_t)(threadIdx.x >> 6)) * a.quad_per_wave + qi;
   const int64_t ray = (qi < a.quad_per_wave && w < a.n_heavy) ? a.order[w] : -1;
   if (ray < 0) return;   // (whole quads: the four lanes share w)
   // a ray frozen at the launch start is frozen_fill_kernel's (the C ABI asks
