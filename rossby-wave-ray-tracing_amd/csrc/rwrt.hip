@@ -1494,9 +1494,28 @@ __device__ __forceinline__ void sin2(double a, double b, double& sa, double& sb)
 __device__ __forceinline__ double cos_small(double x) {
   return k_cos(x);
 }
+// sin(x) for |x| <= 1/16 by its Taylor series to x^7: relative error below
+// 1e-15 there (the x^9 term: 2^-36 / 9! ~ 4e-17, plus rounding)
+__device__ __forceinline__ double sin_small(double x) {
+  const double x2 = x * x;
+  double p = fma(x2, -1.0 / 5040.0, 1.0 / 120.0);
+  p = fma(x2, p, -1.0 / 6.0);
+  return fma(x * x2, p, x);
+}
 __device__ __forceinline__ bool cal_dis_reaches(double lon_c, double lat_c, double lon_p,
                                                 double lat_p, double cos_c, double cos_p,
                                                 double cut_off, double cut_a) {
+  {
+    // a from the polynomial sines is within ~1e-14 relative of the reference's
+    // a (NumPy sines), so a_poly < cut_a (1 - 1e-12) proves a < cut_a -- the
+    // "no jump" verdict below, bit for bit -- without the table sines; any
+    // other lane (larger steps, near the threshold, NaN) takes the exact path.
+    // C3 +1.2 % zonal, +2.1 % non-zonal (profiles/r4/sched/ab_round4.txt)
+    const double x1 = (lat_c - lat_p) / 2.0, x2 = (lon_c - lon_p) / 2.0;
+    const double s1 = sin_small(x1), s2 = sin_small(x2);
+    const double ap = s1 * s1 + (cos_p * cos_c) * (s2 * s2);
+    if (fabs(x1) <= 0.0625 && fabs(x2) <= 0.0625 && ap < cut_a * (1.0 - 1e-12)) return false;
+  }
   double sd, sl;
   sin2((lat_c - lat_p) / 2.0, (lon_c - lon_p) / 2.0, sd, sl);
   const double a = sd * sd + (cos_p * cos_c) * (sl * sl);
@@ -2299,6 +2318,11 @@ __device__ __forceinline__ bool quad_dis_reaches(const QuadRole& R, double lon_c
                                                  double lon_p, double lat_p, double cos_c,
                                                  double cos_p, double cut_off, double cut_a) {
   const double dlat2 = (lat_c - lat_p) / 2.0, dlon2 = (lon_c - lon_p) / 2.0;
+  {   // (cal_dis_reaches' polynomial verdict)
+    const double s1 = sin_small(dlat2), s2 = sin_small(dlon2);
+    const double ap = s1 * s1 + (cos_p * cos_c) * (s2 * s2);
+    if (fabs(dlat2) <= 0.0625 && fabs(dlon2) <= 0.0625 && ap < cut_a * (1.0 - 1e-12)) return false;
+  }
   const double sv = k_sin(R.odd ? dlon2 : dlat2);
   const double sd = qbcast<0>(sv), sl = qbcast<1>(sv);
   const double a = sd * sd + (cos_p * cos_c) * (sl * sl);
