@@ -2432,7 +2432,8 @@ __device__ __forceinline__ void quad_rays(const RunArgs<StaticBG>& a, char* cach
     double ug, vg, cos_c = kNaN;
     bool masked = fabs(y[1]) >= kHalfPi;
     if (!masked) {
-      cos_c = have ? aux[2] : cos_small(y[1]);
+      cos_c = aux[2];
+      if (RARE(!have)) cos_c = cos_small(y[1]);   // (a branch: rare)
       masked = quad_dis_reaches(R, y[0], y[1], prev_lon, prev_lat, cos_c, cos_prev, a.cut_off, a.cut_a);
     }
     if (masked) {
@@ -2574,7 +2575,8 @@ __global__ void __launch_bounds__(256, 1) rk45_run_kernel(RunArgs<BG> a) {
     double ug, vg, cos_c = kNaN;
     bool masked = fabs(y[1]) >= kHalfPi;
     if (!masked) {
-      cos_c = have ? L.aux[2] : cos_small(y[1]);   // |y[1]| < pi/2 or NaN here
+      cos_c = L.aux[2];
+      if (RARE(!have)) cos_c = cos_small(y[1]);   // |y[1]| < pi/2 or NaN here (a branch: rare)
       masked = cal_dis_reaches(y[0], y[1], prev_lon, prev_lat, cos_c, cos_prev, a.cut_off, a.cut_a);
     }
     if (masked) {
