@@ -297,10 +297,12 @@ class RayEngine:
         return torch.sort(key, descending=True, stable=True).indices.to(torch.int64).contiguous()
 
     # a heavy ray's attempt in latency mode / in a loaded rk45_run_kernel wave
-    # (tools/team_latency.py on the heaviest C3 rays: 10.2 us alone in its
-    # wave, 11.5 us at 16 rays per wave, 13.3-13.7 us in the run kernel)
+    # (round 2, tools/team_latency.py on the heaviest C3 rays: 10.2 us alone in
+    # its wave, 11.5 us at 16 rays per wave, 13.3-13.7 us in the run kernel;
+    # round 4, like rays dealt to a wave together: ~9.5-10 us at 16 per wave
+    # against ~13.5, profiles/r4/sched/latency_xcd.txt)
     QUAD_RATIO_1 = 0.76
-    QUAD_RATIO_16 = 0.85
+    QUAD_RATIO_16 = 0.85   # (0.72 picks the same sizes on C3 split 2/4/8 ways: r4mm)
     QUAD_MIN_GAIN = 0.10   # (one C3 GPU: predicted 6-9 %, measured -1 %)
     # rays per wave the auto rule considers: sparser waves measured SLOWER per
     # heavy ray in a full run (tools/team_latency.py --density, 90 d: 16 / 64
