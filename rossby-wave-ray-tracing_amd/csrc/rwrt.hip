@@ -1861,7 +1861,9 @@ struct Lane {
       double sum = y[0];
 #pragma unroll
       for (int v = 1; v < NV; ++v) sum = sum + y[v];
-      if (isnan(sum / (double)NV)) {  // NaN mean: frozen, t := t_bound (rkf45.py:400-403)
+      // NaN mean: frozen, t := t_bound (rkf45.py:400-403); sum / NV is NaN
+      // exactly when sum is (inf / NV = inf, a finite sum stays finite)
+      if (isnan(sum)) {
         t = tb;
         return kFrozen;
       }
@@ -2387,7 +2389,7 @@ __device__ __forceinline__ void quad_rays(const RunArgs<StaticBG>& a, char* cach
     int st = 0;   // 0 step, 1 reached, 2 frozen
     if (!in_step) {
       const double sum = (((y[0] + y[1]) + y[2]) + y[3]) + y[4];
-      if (isnan(sum / 5.0)) {
+      if (isnan(sum)) {   // (== isnan(sum / 5.0): Lane::iterate)
         t = tb;
         st = 2;
       } else if (t == tb) {
