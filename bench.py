@@ -46,6 +46,8 @@ import synthetic as S  # noqa: E402
 METRIC = "ray-steps/sec (whole node), 10^6 rays RKF45; max |Δpos| vs CPU ref"
 BYTES_PER_STEP = 2112          # 6 RHS evals x 4 corners x 11 fields x 8 B
 HBM_PEAK = 8.0e12              # MI355X_MICROARCH.md, chip-level parameters
+FLOP_PER_STEP = 2.0e3          # fp64 FLOP per accepted ray-step (~1462 per attempt x 1.39)
+FP64_PEAK = 78.6e12            # MI355X vector FP64 (16 lanes x FMA per SIMD-cycle x 1024 SIMDs x 2.4 GHz)
 
 
 def c3_rows(bs, lon_offset_deg=0.0, periods=S.C3_PERIODS_DAYS):
@@ -90,16 +92,18 @@ def make_bs(kind="zonal"):
     return bs, bg
 
 
-def cpu_baseline(bg, y0, nrays, days, seed=0, fsal=True):
-    """Time the oracle on ``nrays`` live rays for ``days`` (1 host core).
-    ``fsal=False``: the reference's loop shape (f recomputed for every column
-    at each step start, rkf45.py:378).  Returns (pick, hist, accepted, seconds,
-    nt, rejected, RHS columns evaluated)."""
+def cpu_baseline(bg, y0, nrays, days, seed=0, fsal=True, pick=None):
+    """Time the oracle on ``nrays`` live rays for ``days`` (1 host core) --
+    a random sample, or the rays ``pick``.  ``fsal=False``: the reference's
+    loop shape (f recomputed for every column at each step start,
+    rkf45.py:378).  Returns (pick, hist, accepted, seconds, nt, rejected, RHS
+    columns evaluated)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import rwrt_oracle as O
-    rng = np.random.default_rng(seed)
-    live = np.where(~np.isnan(y0.mean(axis=0)))[0]
-    pick = np.sort(rng.choice(live, size=min(nrays, len(live)), replace=False))
+    if pick is None:
+        rng = np.random.default_rng(seed)
+        live = np.where(~np.isnan(y0.mean(axis=0)))[0]
+        pick = np.sort(rng.choice(live, size=min(nrays, len(live)), replace=False))
     ob = O.Background(**bg)
     nt = int(round(days * 12)) + 1
     cols = [0]
@@ -170,7 +174,8 @@ def find_profile(name, path, workload, schedule):
     return fallback
 
 
-def roofline(steps_per_launch, avg_launch_s, workload, schedule, bytes_per_step, args, bound="valu_issue"):
+def roofline(steps_per_launch, avg_launch_s, workload, schedule, bytes_per_step, args, bound="valu_issue",
+             steps_per_s_gpu=None):
     """The ray-loop kernel against the bound it hits: VALU issue at one wave per
     SIMD.  VALU wave-instructions per launch and the in-kernel clock come from
     the PMC profile of this build and schedule (tools/pmc_valu.py), the launch
@@ -190,6 +195,12 @@ def roofline(steps_per_launch, avg_launch_s, workload, schedule, bytes_per_step,
         out.update(achieved=ach / 1e9, peak=peak / 1e9, frac=ach / peak,
                    valu_insts_per_launch=valu["valu_insts_per_launch"],
                    clock_GHz=valu["clock_hz"] / 1e9,
+                   valu_peak_basis=("4 cycles per wave64 VALU instruction: the SIMD's fp64 rate (16 lanes "
+                                    "per cycle, the 78.6 TF vector FP64 peak) and the one-wave-per-SIMD "
+                                    "issue ceiling of this kernel (256 VGPR + AGPRs, 146 KB LDS per block). "
+                                    "32-bit VALU work issues in 2 cycles when a second wave shares the "
+                                    "SIMD (MI355X_MICROARCH.md:54,473), so against the chip's mixed-width "
+                                    "ceiling this frac is an upper bound"),
                    note=("one wave per SIMD (256 VGPR + AGPRs, 146 KB LDS per block): every VALU "
                          "wave-instruction holds its SIMD's issue for >= 4 cycles; peak = 1024 SIMDs x "
                          "in-kernel clock (GRBM_GUI_ACTIVE / 8 / kernel time) / 4"))
@@ -204,9 +215,18 @@ def roofline(steps_per_launch, avg_launch_s, workload, schedule, bytes_per_step,
                   "frac": traffic["traffic_bytes_per_launch"] / avg_launch_s / HBM_PEAK if traffic else None,
                   "unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)"}
     out["algorithmic"] = {"bytes_per_ray_step": bytes_per_step, "GBps": alg / 1e9,
+                          "frac_of_hbm_peak": alg / HBM_PEAK,
+                          "bound": "none: not an HBM bound (>= 1 by construction at 2.5 degrees)",
                           "note": ("SURVEY.md 8(d): 6 RHS x 4 corners x 11 fields x 8 B per accepted step; "
                                    "most lookups are served by the per-lane LDS cell cache and L2, so this "
                                    "is a yardstick, not HBM traffic, and can exceed the HBM peak")}
+    if steps_per_s_gpu is not None:
+        # the arithmetic the path needs, against the vector FP64 peak
+        out["fp64_flop_frac"] = steps_per_s_gpu * FLOP_PER_STEP / FP64_PEAK
+        out["fp64_flop"] = {"flop_per_ray_step": FLOP_PER_STEP, "TFLOPs": steps_per_s_gpu * FLOP_PER_STEP / 1e12,
+                            "peak_TFLOPs": FP64_PEAK / 1e12,
+                            "note": "SURVEY.md 8(d): ~1462 fp64 FLOP per DP5(4) attempt x 1.39 attempts per "
+                                    "accepted step, transcendentals excluded; per GPU"}
     if bound == "hbm":
         # C5: the 0.25-degree levels are gathered from HBM / MALL (one level per
         # lane cached in LDS): the memory roofline leads, VALU issue beside it
@@ -422,7 +442,7 @@ def main():
     if args.config == "C5":
         return main_c5(args, dist, group, rank, world, dev, share)
     from engine import RayEngine
-    from shard import run_sharded
+    from shard import broadcast_array, run_sharded
     weak = args.scaling == "weak"
     bs, bg = make_bs(args.bg)
     periods = S.C3_PERIODS_DAYS[: args.periods]
@@ -434,7 +454,11 @@ def main():
     t_init = time.perf_counter() - t_init
     if args.replicate > 1:
         y0 = np.concatenate([y0] * args.replicate, axis=1)
-    eng = RayEngine.from_bs(bs, device=dev)
+    # the basic state every rank integrates through is rank 0's (bs.py:202-262
+    # reads its file on one process): its field stack broadcast before the
+    # timed steps, then rank 0's packed state again inside every step
+    fields = broadcast_array(bs.fields if rank == 0 else None, group=group) if dist else bs.fields
+    eng = RayEngine(fields, bs.lon, bs.lat, device=dev)
     nt = int(round(args.days * 12)) + 1
     gpu_init = args.replicate == 1
     init_same = None
@@ -586,7 +610,8 @@ def main():
                                   "threshold": eng.SPLIT_RHO, "rows": eng.SPLIT_ROWS},
             "library": os.path.basename(os.environ.get("RWRT_LIB", "librwrt.so")),
             "library_sha256": library_sha(),
-            "roofline": roofline(per_launch_steps, avg_launch_s, workload, schedule, BYTES_PER_STEP, args),
+            "roofline": roofline(per_launch_steps, avg_launch_s, workload, schedule, BYTES_PER_STEP, args,
+                                 steps_per_s_gpu=value / world),
         }
         if weak and "all" in gathered:
             result["gathered_endpoints"] = {
@@ -594,10 +619,10 @@ def main():
                 "alive_at_end": int(sum(int((~torch.isnan(b[:, 0])).sum().item()) for b in gathered["all"]))}
         if world == 1 and not args.no_cpu:
             pick, hist, csteps, cdt, cnt, crej, ccols = cpu_baseline(bg, y0, args.cpu_rays, args.cpu_days)
-            # the reference's own loop shape, timed on half the sample (the same
-            # rays' first half; ~2x the RHS work per step)
+            # the reference's own loop shape, timed on the first half of the
+            # same sample (~2x the RHS work per step)
             rpick, _, rsteps, rdt, _, _, rcols = cpu_baseline(bg, y0, args.cpu_rays // 2, args.cpu_days,
-                                                               seed=2, fsal=False)
+                                                               fsal=False, pick=pick[: len(pick) // 2])
             result["cpu_baseline"] = {
                 "value": rsteps / rdt, "unit": "ray-steps/s", "cores": 1, "kind": "reference_loop",
                 "sample": f"{len(rpick)} live C3 rays x {args.cpu_days:g} d ({rsteps} ray-steps, {rdt:.1f} s) "
@@ -644,7 +669,7 @@ def main():
                 "identical_values_frac": float(same.mean()),
                 "rays_identical_all_rows": int(same.all(axis=(0, 1)).sum()),
                 "note": "GPU rows vs the oracle (NumPy, the reference's arithmetic) on the cpu_baseline sample"}
-        if weak:
+        if weak and world > 1:
             # not a BASELINE config (N x the C3 set): the aggregate rides under
             # its own key; the line's value stays empty
             result["weak_scaling"] = {"value": value, "unit": "ray-steps/s",
@@ -655,6 +680,10 @@ def main():
     if dist:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def backend_of(dist):
+    return dist.get_backend() if dist is not None and dist.is_initialized() else None
 
 
 def c5_parity_sample(eng, rows_all, fields, dev):
@@ -705,18 +734,21 @@ def main_c5(args, dist, group, rank, world, dev, share=1):
     snapshots)."""
     from engine import RayEngine
     from levels import Levels
-    from shard import run_sharded
+    from shard import broadcast_levels, run_sharded
     res, dt_bg = 0.25, 6 * 3600.0
     nt = int(round(args.days * 12)) + 1
     nlev = int(np.ceil((nt - 1) * 7200.0 / dt_bg)) + 1
-    b0 = S.background_level(0, res=res)
+    b0 = S.background_level(0, res=res)     # (the axes; every rank knows the grid)
     t_build = time.perf_counter()
     lv = Levels(b0["lat"], b0["lon"], nlev, t0=0.0, dt=dt_bg, fp32=(args.fields in ("fp32", "fp32a")), device=dev,
                 arith32=(args.fields == "fp32a"))
-    for j in range(nlev):
+
+    def make_uv(j):   # rank 0 only: the snapshots a real run reads from its file there
         bj = b0 if j == 0 else S.background_level(j, res=res)
-        lv.set_level(j, bj["u"], bj["v"])
-    torch.cuda.synchronize()
+        return bj["u"], bj["v"]
+    # rank 0's u, v snapshots broadcast (RCCL over xGMI; gloo when ranks share a
+    # GPU), every rank building its packed levels: outside the timed step
+    bcast = broadcast_levels(lv, make_uv, group=group if dist else None)
     t_build = time.perf_counter() - t_build
     eng = RayEngine.from_levels(lv)
     cfg = S.config("C5")
@@ -815,10 +847,15 @@ def main_c5(args, dist, group, rank, world, dev, share=1):
             "ray_steps_per_step": tot_steps / args.steps,
             "rejected_per_accepted": tot_rej * args.steps / max(tot_steps, 1),
             "levels_build_s": t_build,
+            "levels_broadcast": dict(bcast, backend=backend_of(dist),
+                                     note="rank 0's u, v snapshots (float32) broadcast in blocks of 16 levels, "
+                                          "each rank building its packed levels with rwrt_bs_ready; before "
+                                          "the timed steps (bs.py:202-262 reads the file on one process)"),
             "queue_order": args.order,
             "library_sha256": library_sha(),
             "init": "GPU rwrt_ray_initial inside every timed step",
-            "roofline": roofline(per_launch_steps, avg_launch_s, workload, schedule, bps, args, bound="hbm")}
+            "roofline": roofline(per_launch_steps, avg_launch_s, workload, schedule, bps, args, bound="hbm",
+                                 steps_per_s_gpu=tot_steps / max_el / world)}
         if weak and world > 1:
             c5_line["weak_scaling"] = {"value": c5_line["value"], "unit": "ray-steps/s",
                                        "note": f"{world} x the C5 set: a diagnostic, not BASELINE configs[4]"}

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RWRT_ABI_VERSION 2
+#define RWRT_ABI_VERSION 3  /* 3: constant row tails (rwrt_rk45_run_tails, rwrt_expand_tails) */
 #define RWRT_NFIELD_REF 18  /* BS.fields[..., 18]            (bs.py:349-368) */
 #define RWRT_NFIELD_PACK 12 /* 11 hot fields + 1 pad per grid point           */
 #define RWRT_NVAR 5         /* y = (lon, lat, k, l, amp)     (wr.py:768-776)  */
@@ -203,6 +203,38 @@ rwrt_status rwrt_rk45_run(rwrt_ctx* ctx, const rwrt_grid* g, const double* d_pac
                           int32_t* d_nanrow, double* d_out, int32_t* d_work,
                           void* stream);
 
+/* rwrt_rk45_run with constant row tails (ABI 3).  A ray frozen at the call's
+ * start (a NaN in its state, rkf45.py:400-403: dead root slots, rays masked
+ * by wr.py:838-850 in an earlier call) repeats one row for the whole call
+ * (wr.py:868-876 stores the unchanged state).  Instead of writing that row
+ * into d_out for every row, the call stores it once:
+ *  d_tail_from[nray] (int32): the first row i (it_begin <= i <= it_end) from
+ *    which ray j's rows of this call all equal d_tail_row[j] and are NOT
+ *    written to d_out; it_end when the ray has no constant tail (every row of
+ *    it is in d_out).  This build gives the rays frozen at the call's start
+ *    it_begin and every other ray it_end (a ray that freezes during the call
+ *    writes its remaining rows, as rwrt_rk45_run does).
+ *  d_tail_row[nray][8] (16-byte aligned): the tail row of ray j (meaningful
+ *    where d_tail_from[j] < it_end).
+ * rwrt_expand_tails writes the tails into d_out for a consumer that wants the
+ * rows dense: then d_out equals rwrt_rk45_run's bit for bit, as do the state,
+ * counters and nanrow after every call.  NULL d_tail_from and d_tail_row:
+ * rwrt_rk45_run itself.  (C3: 116 GB of constant rows per 90-day step that
+ * are never written.) */
+rwrt_status rwrt_rk45_run_tails(rwrt_ctx* ctx, const rwrt_grid* g, const double* d_packed,
+                                int64_t nray, const rwrt_params* p,
+                                const double* d_tbound, int32_t it_begin,
+                                int32_t it_end, const int64_t* d_order,
+                                int64_t n_heavy, double* d_state, int64_t* d_count,
+                                int32_t* d_nanrow, double* d_out, int32_t* d_tail_from,
+                                double* d_tail_row, int32_t* d_work, void* stream);
+/* d_out[(j*(it_end-it_begin) + r)*8 + 0..7] := d_tail_row[j][0..7] for every
+ * ray j and row it_begin + r >= d_tail_from[j] (the dense rows of a tails
+ * call); other rows are not touched. */
+rwrt_status rwrt_expand_tails(int64_t nray, int32_t it_begin, int32_t it_end,
+                              const int32_t* d_tail_from, const double* d_tail_row,
+                              double* d_out, void* stream);
+
 /* Fixed-step RK4 ray loop, the reference's default integrator:
  * WR.core_ray_run_numpy (wr.py:702-765) with rk4_step_numpy (wr.py:583-622)
  * and core_rk4_step (wr.py:89-95), for rows it_begin <= i < it_end, dt =
@@ -250,6 +282,14 @@ rwrt_status rwrt_rk45_run_tv(rwrt_ctx* ctx, const rwrt_grid* g, const rwrt_backg
                              int64_t n_heavy, double* d_state, int64_t* d_count,
                              int32_t* d_nanrow, double* d_out, int32_t* d_work,
                              void* stream);
+/* rwrt_rk45_run_tv with constant row tails (as rwrt_rk45_run_tails). */
+rwrt_status rwrt_rk45_run_tv_tails(rwrt_ctx* ctx, const rwrt_grid* g, const rwrt_background* b,
+                                   int64_t nray, const rwrt_params* p,
+                                   const double* d_tbound, int32_t it_begin,
+                                   int32_t it_end, const int64_t* d_order,
+                                   int64_t n_heavy, double* d_state, int64_t* d_count,
+                                   int32_t* d_nanrow, double* d_out, int32_t* d_tail_from,
+                                   double* d_tail_row, int32_t* d_work, void* stream);
 /* The time-varying RHS at per-point times: d_t[n], d_y[5][n] -> d_dydt[5][n]. */
 rwrt_status rwrt_rhs_tv(const rwrt_grid* g, const rwrt_background* b, int64_t n,
                         const double* d_t, const double* d_y, double* d_dydt,
@@ -274,8 +314,11 @@ rwrt_status rwrt_kat_rk45(int32_t kind, int64_t ncol, const double* d_y0,
  * division pair (as its first / second quotient), 25/26/27/28 the reference
  * NumPy's sin/cos/tan/power as restated in csrc/np_math.h, 29 the restated
  * VRCP14PD, 30/31/32 sin/cos/tan and 33 pow exactly as the kernels evaluate
- * them, 34 x / y by the RHS's shared-reciprocal division (qdiv) and 35 1.0
- * where that division is inside its exact range (DivGuard), else 0.0.
+ * them, 34 x / y by the RHS's shared-reciprocal division (qdiv), 35 1.0
+ * where that division is inside its exact range (DivGuard), else 0.0, and
+ * 36/37 the jump mask's verdict (wr.py:844-850; 1.0: a jump) for a step of
+ * (dlat, dlon) = (x, y) from (lon, lat) = (1.0, 0.6) rad at cut_off 0.05 rad,
+ * 36 with the kernels' polynomial "no jump" shortcut, 37 without it.
  * Lets the tests prove which operations are bit-exact on the GPU (IEEE
  * division, sqrt, fmod) and measure the last-bit agreement of the rest. */
 rwrt_status rwrt_selftest_math(int32_t kind, int64_t n, const double* d_x,

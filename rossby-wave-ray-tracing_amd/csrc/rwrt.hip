@@ -433,6 +433,10 @@ __device__ __forceinline__ void lds_dma_wait() { asm volatile("s_waitcnt vmcnt(0
 // ordered to match (CachedStaticBG::refill): chunks 0-3 of every corner
 // first, so the first reads wait for part of it only.
 constexpr int kCacheAhead = 1;
+// end() reads chunks 0..kCacheAhead after waiting for the refill's first 16
+// loads only (chunks 0-3, vmcnt(8)); the wait for all 24 sits before the
+// read of chunk 4 -- a read-ahead of 4 or more would read chunk 4 early
+static_assert(kCacheAhead >= 0 && kCacheAhead < 4, "end() prologue waits for chunks 0-3 only");
 #ifndef RWRT_KAP_IN_LOOKUP   // the wavenumber terms under the cell cache's first reads: +0.3 % (r4e)
 #define RWRT_KAP_IN_LOOKUP 1
 #endif
@@ -1502,15 +1506,19 @@ __device__ __forceinline__ double sin_small(double x) {
   p = fma(x2, p, -1.0 / 6.0);
   return fma(x * x2, p, x);
 }
+template <bool kFast = true>
 __device__ __forceinline__ bool cal_dis_reaches(double lon_c, double lat_c, double lon_p,
                                                 double lat_p, double cos_c, double cos_p,
                                                 double cut_off, double cut_a) {
-  {
+  if (kFast) {
     // a from the polynomial sines is within ~1e-14 relative of the reference's
     // a (NumPy sines), so a_poly < cut_a (1 - 1e-12) proves a < cut_a -- the
     // "no jump" verdict below, bit for bit -- without the table sines; any
     // other lane (larger steps, near the threshold, NaN) takes the exact path.
-    // C3 +1.2 % zonal, +2.1 % non-zonal (profiles/r4/sched/ab_round4.txt)
+    // C3 +1.2 % zonal, +2.1 % non-zonal (profiles/r4/sched/ab_round4.txt).
+    // quad_dis_reaches repeats these operations; tests/test_gpu_parity.py
+    // (selftest kinds 36/37) checks the verdict with and without them on
+    // steps straddling the threshold.
     const double x1 = (lat_c - lat_p) / 2.0, x2 = (lon_c - lon_p) / 2.0;
     const double s1 = sin_small(x1), s2 = sin_small(x2);
     const double ap = s1 * s1 + (cos_p * cos_c) * (s2 * s2);
@@ -2040,6 +2048,18 @@ struct RunArgs {
   int64_t trace_cap = 0;
 };
 
+
+// A frozen ray's rows are all one row (rkf45.py:400-403: its state never
+// changes again): with tails, that row is stored once per ray instead
+__device__ __forceinline__ void store_tail(double* tail_row, int64_t ray, double2 r0, double2 r1, double2 r2,
+                                           double2 r3) {
+  double2* o = reinterpret_cast<double2*>(tail_row + (size_t)ray * RWRT_NOUT);
+  o[0] = r0;
+  o[1] = r1;
+  o[2] = r2;
+  o[3] = r3;
+}
+
 // rwrt_ctx_set_trace: where (HW_ID, XCC) and when a traced ray ran
 constexpr int kTraceWords = 10;
 __device__ __forceinline__ void trace_start(int64_t* tr, int64_t w) {
@@ -2320,7 +2340,7 @@ __device__ __forceinline__ bool quad_dis_reaches(const QuadRole& R, double lon_c
                                                  double lon_p, double lat_p, double cos_c,
                                                  double cos_p, double cut_off, double cut_a) {
   const double dlat2 = (lat_c - lat_p) / 2.0, dlon2 = (lon_c - lon_p) / 2.0;
-  {   // (cal_dis_reaches' polynomial verdict)
+  {   // (cal_dis_reaches' polynomial verdict, the same operations: selftest kinds 36/37)
     const double s1 = sin_small(dlat2), s2 = sin_small(dlon2);
     const double ap = s1 * s1 + (cos_p * cos_c) * (s2 * s2);
     if (fabs(dlat2) <= 0.0625 && fabs(dlon2) <= 0.0625 && ap < cut_a * (1.0 - 1e-12)) return false;
@@ -2656,13 +2676,19 @@ __global__ void __launch_bounds__(256, 1) rk45_run_kernel(RunArgs<BG> a) {
 // 16-B stores.
 // ---------------------------------------------------------------------------
 __global__ void frozen_flag_kernel(const double* __restrict__ state, int64_t nray,
-                                   uint8_t* __restrict__ frozen) {
+                                   uint8_t* __restrict__ frozen, int32_t* __restrict__ tail_from = nullptr,
+                                   int32_t it_begin = 0, int32_t it_end = 0) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nray;
        i += (int64_t)gridDim.x * blockDim.x) {
     double sum = state[i];
 #pragma unroll
     for (int v = 1; v < 5; ++v) sum = sum + state[v * nray + i];
-    frozen[i] = isnan(sum / 5.0) ? 1 : 0;   // Lane::iterate's NaN-mean test
+    const bool frz = isnan(sum / 5.0);   // Lane::iterate's NaN-mean test
+    frozen[i] = frz ? 1 : 0;
+    // tails: a frozen ray's tail starts at the launch (its row: frozen_tail_kernel);
+    // the others have none (a ray that freezes inside the launch writes its
+    // remaining rows as before: rare, and the ray loops stay as they are)
+    if (tail_from) tail_from[i] = frz ? it_begin : it_end;
   }
 }
 
@@ -2699,17 +2725,12 @@ __device__ __forceinline__ void write_frozen_tile(double* out, int64_t base, int
   }
 }
 
+// The row of a ray frozen at the launch start: rk45_run_kernel's fetch +
+// kFrozen iteration + post-processing, verbatim (and its state update)
 template <class BG>
-__global__ void __launch_bounds__(kFillThreads) __attribute__((amdgpu_num_vgpr(128)))
-frozen_fill_kernel(RunArgs<BG> a) {
-  nm_stage<NM_SINCOS>();
-  const int64_t nrows = a.it_end - a.it_begin;
-  const int64_t base = blockIdx.x * (int64_t)kFillThreads;
-  const int64_t ray = base + threadIdx.x;
-  const bool mine = ray < a.nray && a.frozen[ray];
-  double2 r0 = make_double2(0.0, 0.0), r1 = r0, r2 = r0, r3 = r0;
-  if (mine) {
-    // rk45_run_kernel's fetch + kFrozen iteration + post-processing, verbatim
+__device__ __forceinline__ void frozen_row(const RunArgs<BG>& a, int64_t ray, double2& r0, double2& r1,
+                                           double2& r2, double2& r3) {
+  {
     double y[5];
 #pragma unroll
     for (int v = 0; v < 5; ++v) y[v] = a.state[v * a.nray + ray];
@@ -2742,12 +2763,58 @@ frozen_fill_kernel(RunArgs<BG> a) {
     a.state[10 * a.nray + ray] = a.tbound[a.it_end - 1];
     a.nanrow[ray] = nanrow;
   }
+}
+
+template <class BG>
+__global__ void __launch_bounds__(kFillThreads) __attribute__((amdgpu_num_vgpr(128)))
+frozen_fill_kernel(RunArgs<BG> a) {
+  nm_stage<NM_SINCOS>();
+  const int64_t nrows = a.it_end - a.it_begin;
+  const int64_t base = blockIdx.x * (int64_t)kFillThreads;
+  const int64_t ray = base + threadIdx.x;
+  const bool mine = ray < a.nray && a.frozen[ray];
+  double2 r0 = make_double2(0.0, 0.0), r1 = r0, r2 = r0, r3 = r0;
+  if (mine) frozen_row(a, ray, r0, r1, r2, r3);
   write_frozen_tile(a.out, base, nrows, mine, r0, r1, r2, r3);
+}
+
+// With tails (rwrt_rk45_run_tails) a frozen ray's rows are ONE row: this
+// kernel stores each flagged ray's row as its constant tail from it_begin,
+// on the side stream beside the run kernel like frozen_fill_kernel (the
+// same register and LDS caps) -- 64 B per frozen ray instead of 64 B per
+// frozen ray and row (C3: 116 GB of constant rows per 90-day step, which
+// frozen_fill_kernel wrote beside the ray loop, competing for its memory
+// queues).  rwrt_expand_tails materialises the rows for consumers that want
+// them dense.
+template <class BG>
+__global__ void __launch_bounds__(kFillThreads) __attribute__((amdgpu_num_vgpr(128)))
+frozen_tail_kernel(RunArgs<BG> a, double* __restrict__ tail_row) {
+  nm_stage<NM_SINCOS>();
+  const int64_t ray = blockIdx.x * (int64_t)kFillThreads + threadIdx.x;
+  if (ray < a.nray && a.frozen[ray]) {
+    double2 r0, r1, r2, r3;
+    frozen_row(a, ray, r0, r1, r2, r3);
+    store_tail(tail_row, ray, r0, r1, r2, r3);   // (tail_from: frozen_flag_kernel)
+  }
+}
+
+// rwrt_expand_tails: rows [tail_from[j], it_end) of every ray j := tail_row[j],
+// one 16-B quarter of a row per thread (coalesced; rows without a tail untouched)
+__global__ void expand_tails_kernel(double* __restrict__ out, int64_t nray, int32_t it_begin, int32_t nrows,
+                                    const int32_t* __restrict__ tail_from, const double* __restrict__ tail_row) {
+  const int64_t per = (int64_t)nrows * 4, n = nray * per;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t j = i / per;
+    const int64_t q = i - j * per;
+    if (it_begin + (int32_t)(q >> 2) >= tail_from[j])
+      reinterpret_cast<double2*>(out)[i] = reinterpret_cast<const double2*>(tail_row)[j * 4 + (q & 3)];
+  }
 }
 
 
 __global__ void math_kernel(int kind, int64_t n, const double* __restrict__ x,
-                            const double* __restrict__ y, double* __restrict__ out) {
+                            const double* __restrict__ y, double* __restrict__ out,
+                            double cut_a = 0.0) {
   nm_stage<NM_ALL>();
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -2788,6 +2855,15 @@ __global__ void math_kernel(int kind, int64_t n, const double* __restrict__ x,
       G.num(a);
       G.den(b);
       r = G.ok() ? 1.0 : 0.0;
+    } break;
+    case 36:     // the jump mask's verdict (1: jump) for a step of (dlat, dlon) = (a, b) from
+    case 37: {   // (lon, lat) = (1.0, 0.6), cut_off 0.05 rad: 36 with the fast verdict, 37 without
+      const double lat_p = 0.6, lon_p = 1.0, cut = 0.05;
+      const double lat_c = lat_p + a, lon_c = lon_p + b;
+      const double cp = k_cos(lat_p), cc = k_cos(lat_c), ca = cut_a;   // haversine_cut(0.05), host
+      const bool j = (kind == 36) ? cal_dis_reaches<true>(lon_c, lat_c, lon_p, lat_p, cc, cp, cut, ca)
+                                  : cal_dis_reaches<false>(lon_c, lat_c, lon_p, lat_p, cc, cp, cut, ca);
+      r = j ? 1.0 : 0.0;
     } break;
     default: r = kNaN; break;   // (unreachable: rwrt_selftest_math rejects other kinds)
   }
@@ -3298,7 +3374,8 @@ template <class BG>
 rwrt_status launch_run(rwrt_ctx* ctx, const BG& B, int64_t nray, const rwrt_params* p,
                        const double* d_tbound, int32_t it_begin, int32_t it_end,
                        const int64_t* d_order, int64_t n_heavy, double* d_state, int64_t* d_count,
-                       int32_t* d_nanrow, double* d_out, int32_t* d_work, void* stream) {
+                       int32_t* d_nanrow, double* d_out, int32_t* d_tail_from, double* d_tail_row,
+                       int32_t* d_work, void* stream) {
   if (rwrt_status s = ctx_check(ctx)) return s;
   if (!p) return fail(RWRT_ERR_ARG, "params is NULL%s");
   if (nray < 0 || nray > 0x7fffffffLL) return fail(RWRT_ERR_ARG, "nray out of range%s");
@@ -3308,6 +3385,9 @@ rwrt_status launch_run(rwrt_ctx* ctx, const BG& B, int64_t nray, const rwrt_para
     return fail(RWRT_ERR_ARG, "NULL buffer to rwrt_rk45_run%s");
   if (reinterpret_cast<uintptr_t>(d_out) % 16 != 0)
     return fail(RWRT_ERR_ARG, "output rows must be 16-byte aligned%s");
+  if (!d_tail_from != !d_tail_row) return fail(RWRT_ERR_ARG, "tails need both d_tail_from and d_tail_row%s");
+  if (reinterpret_cast<uintptr_t>(d_tail_row) % 16 != 0)
+    return fail(RWRT_ERR_ARG, "tail rows must be 16-byte aligned%s");
   if (nray == 0) return RWRT_OK;
   if (n_heavy < 0 || n_heavy > nray) return fail(RWRT_ERR_ARG, "n_heavy out of range%s");
   if (n_heavy > 0 && !d_order) return fail(RWRT_ERR_ARG, "n_heavy > 0 needs d_order%s");
@@ -3338,12 +3418,14 @@ rwrt_status launch_run(rwrt_ctx* ctx, const BG& B, int64_t nray, const rwrt_para
                 n_heavy, 0, haversine_cut(p->cut_off), nullptr};
   // frozen rays: flagged on `stream`, filled on the context's side stream
   // while the run kernel (which skips them) integrates the rest; `stream` then
-  // waits for the fill, so the call stays one stream-ordered operation
+  // waits for the fill, so the call stays one stream-ordered operation.  With
+  // tails, the side stream stores their constant tail rows instead of
+  // filling (frozen_tail_kernel).
   if (rwrt_status s = ctx_flags(ctx, nray)) return s;
   a.frozen = ctx->flags;
   if (rwrt_status s = ctx_begin(ctx, st, [&] {
         hipLaunchKernelGGL(frozen_flag_kernel, dim3(grid_for(nray, 256)), dim3(256), 0, st, d_state, nray,
-                           ctx->flags);
+                           ctx->flags, d_tail_from, it_begin, it_end);
       }))
     return s;
   if constexpr (std::is_same<BG, StaticBG>::value) {
@@ -3369,9 +3451,13 @@ rwrt_status launch_run(rwrt_ctx* ctx, const BG& B, int64_t nray, const rwrt_para
     }
     if (rwrt_status s = check_launch("rk45_run_kernel")) return s;
   }
-  hipLaunchKernelGGL(frozen_fill_kernel<BG>, dim3((unsigned)((nray + kFillThreads - 1) / kFillThreads)),
-                     dim3(kFillThreads), 0, ctx->side, a);
-  if (rwrt_status s = check_launch("frozen_fill_kernel")) return s;
+  if (d_tail_from)
+    hipLaunchKernelGGL(frozen_tail_kernel<BG>, dim3((unsigned)((nray + kFillThreads - 1) / kFillThreads)),
+                       dim3(kFillThreads), 0, ctx->side, a, d_tail_row);
+  else
+    hipLaunchKernelGGL(frozen_fill_kernel<BG>, dim3((unsigned)((nray + kFillThreads - 1) / kFillThreads)),
+                       dim3(kFillThreads), 0, ctx->side, a);
+  if (rwrt_status s = check_launch(d_tail_from ? "frozen_tail_kernel" : "frozen_fill_kernel")) return s;
   return ctx_end(ctx, st);
 }
 
@@ -3523,7 +3609,7 @@ using namespace rwrt;
 
 extern "C" {
 
-const char* rwrt_version(void) { return "rwrt 0.2 (gfx950, abi 2)"; }
+const char* rwrt_version(void) { return "rwrt 0.3 (gfx950, abi 3)"; }
 
 rwrt_status rwrt_ctx_create(int32_t device, rwrt_ctx** out) {
   if (!out) return fail(RWRT_ERR_ARG, "out is NULL%s");
@@ -3669,10 +3755,33 @@ rwrt_status rwrt_rk45_run(rwrt_ctx* ctx, const rwrt_grid* g, const double* d_pac
                           int32_t it_begin, int32_t it_end, const int64_t* d_order,
                           int64_t n_heavy, double* d_state, int64_t* d_count, int32_t* d_nanrow,
                           double* d_out, int32_t* d_work, void* stream) {
+  return rwrt_rk45_run_tails(ctx, g, d_packed, nray, p, d_tbound, it_begin, it_end, d_order, n_heavy, d_state,
+                             d_count, d_nanrow, d_out, nullptr, nullptr, d_work, stream);
+}
+
+rwrt_status rwrt_rk45_run_tails(rwrt_ctx* ctx, const rwrt_grid* g, const double* d_packed,
+                                int64_t nray, const rwrt_params* p, const double* d_tbound,
+                                int32_t it_begin, int32_t it_end, const int64_t* d_order,
+                                int64_t n_heavy, double* d_state, int64_t* d_count, int32_t* d_nanrow,
+                                double* d_out, int32_t* d_tail_from, double* d_tail_row, int32_t* d_work,
+                                void* stream) {
   Field F;
   if (rwrt_status s = make_field(g, d_packed, F)) return s;
   return launch_run(ctx, StaticBG{F}, nray, p, d_tbound, it_begin, it_end, d_order, n_heavy, d_state,
-                    d_count, d_nanrow, d_out, d_work, stream);
+                    d_count, d_nanrow, d_out, d_tail_from, d_tail_row, d_work, stream);
+}
+
+rwrt_status rwrt_expand_tails(int64_t nray, int32_t it_begin, int32_t it_end, const int32_t* d_tail_from,
+                              const double* d_tail_row, double* d_out, void* stream) {
+  if (nray < 0 || it_begin >= it_end) return fail(RWRT_ERR_ARG, "bad rwrt_expand_tails shape%s");
+  if (nray == 0) return RWRT_OK;
+  if (!d_tail_from || !d_tail_row || !d_out) return fail(RWRT_ERR_ARG, "NULL buffer to rwrt_expand_tails%s");
+  if (reinterpret_cast<uintptr_t>(d_out) % 16 != 0 || reinterpret_cast<uintptr_t>(d_tail_row) % 16 != 0)
+    return fail(RWRT_ERR_ARG, "rows must be 16-byte aligned%s");
+  const int64_t n = nray * (int64_t)(it_end - it_begin) * 4;
+  hipLaunchKernelGGL(expand_tails_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, d_out,
+                     nray, it_begin, it_end - it_begin, d_tail_from, d_tail_row);
+  return check_launch("expand_tails_kernel");
 }
 
 rwrt_status rwrt_rk45_init_tv(const rwrt_grid* g, const rwrt_background* b, int64_t nray,
@@ -3699,22 +3808,31 @@ rwrt_status rwrt_rk45_run_tv(rwrt_ctx* ctx, const rwrt_grid* g, const rwrt_backg
                              int32_t it_end, const int64_t* d_order, int64_t n_heavy,
                              double* d_state, int64_t* d_count, int32_t* d_nanrow, double* d_out,
                              int32_t* d_work, void* stream) {
+  return rwrt_rk45_run_tv_tails(ctx, g, b, nray, p, d_tbound, it_begin, it_end, d_order, n_heavy, d_state,
+                                d_count, d_nanrow, d_out, nullptr, nullptr, d_work, stream);
+}
+
+rwrt_status rwrt_rk45_run_tv_tails(rwrt_ctx* ctx, const rwrt_grid* g, const rwrt_background* b,
+                                   int64_t nray, const rwrt_params* p, const double* d_tbound,
+                                   int32_t it_begin, int32_t it_end, const int64_t* d_order, int64_t n_heavy,
+                                   double* d_state, int64_t* d_count, int32_t* d_nanrow, double* d_out,
+                                   int32_t* d_tail_from, double* d_tail_row, int32_t* d_work, void* stream) {
   if (b && b->fp32 == 2) {
     VaryingBGA32 B;
     if (rwrt_status s = make_varying(g, b, static_cast<VaryingBG<float>&>(B))) return s;
     return launch_run(ctx, B, nray, p, d_tbound, it_begin, it_end, d_order, n_heavy, d_state, d_count,
-                      d_nanrow, d_out, d_work, stream);
+                      d_nanrow, d_out, d_tail_from, d_tail_row, d_work, stream);
   }
   if (b && b->fp32) {
     VaryingBG<float> B;
     if (rwrt_status s = make_varying(g, b, B)) return s;
     return launch_run(ctx, B, nray, p, d_tbound, it_begin, it_end, d_order, n_heavy, d_state, d_count,
-                      d_nanrow, d_out, d_work, stream);
+                      d_nanrow, d_out, d_tail_from, d_tail_row, d_work, stream);
   }
   VaryingBG<double> B;
   if (rwrt_status s = make_varying(g, b, B)) return s;
   return launch_run(ctx, B, nray, p, d_tbound, it_begin, it_end, d_order, n_heavy, d_state, d_count,
-                    d_nanrow, d_out, d_work, stream);
+                    d_nanrow, d_out, d_tail_from, d_tail_row, d_work, stream);
 }
 
 rwrt_status rwrt_rhs_tv(const rwrt_grid* g, const rwrt_background* b, int64_t n,
@@ -3824,13 +3942,14 @@ rwrt_status rwrt_kat_rk45(int32_t kind, int64_t ncol, const double* d_y0, int32_
 
 rwrt_status rwrt_selftest_math(int32_t kind, int64_t n, const double* d_x, const double* d_y,
                                double* d_out, void* stream) {
-  if (n < 0 || kind < 0 || kind > 35 || (n > 0 && (!d_x || !d_out)))
+  if (n < 0 || kind < 0 || kind > 37 || (n > 0 && (!d_x || !d_out)))
     return fail(RWRT_ERR_ARG, "bad selftest arguments%s");
   if (kind >= 17 && kind <= 22)   // retired device-libm restatements: never alias another kind
     return fail(RWRT_ERR_ARG, "selftest kinds 17-22 are retired%s");
   if (n == 0) return RWRT_OK;
+  if (kind >= 36 && !d_y) return fail(RWRT_ERR_ARG, "selftest kinds 36/37 need d_y%s");
   hipLaunchKernelGGL(math_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, kind,
-                     n, d_x, d_y, d_out);
+                     n, d_x, d_y, d_out, haversine_cut(0.05));
   return check_launch("math_kernel");
 }
 

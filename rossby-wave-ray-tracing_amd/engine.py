@@ -49,8 +49,45 @@ class RunResult:
         return int(self.nacc.sum().item())
 
 
+class Tails:
+    """The constant row tails of one ray-loop launch (``rwrt_rk45_run_tails``,
+    include/rwrt.h): ray j's rows from ``frm[j]`` (int32, in [i0, i1]; i1 = no
+    tail) to the launch's end all equal ``row[j]`` (``[nray, 8]``) and are not
+    in the launch's row buffer.  A frozen ray (rkf45.py:400-403) repeats one
+    row, so 70 % of C3's output rows are never written; ``RayEngine.expand``
+    writes them for a consumer that wants the rows dense."""
+
+    def __init__(self, nray, device):
+        self.frm = torch.empty(nray, dtype=torch.int32, device=device)
+        self.row = torch.empty((nray, H.NOUT), dtype=F64, device=device)
+
+    def take(self, idx):
+        t = Tails.__new__(Tails)
+        t.frm, t.row = self.frm[idx].contiguous(), self.row[idx].contiguous()
+        return t
+
+    def last_row(self, view, i1):
+        """Each ray's last row of the launch ``[i0, i1)`` whose rows are ``view``."""
+        return torch.where((self.frm < i1)[:, None], self.row, view[:, -1])
+
+
+def deliver(eng, sink, i0, i1, view, tails):
+    """Hand a launch's rows to ``sink``: with its tails when the sink takes
+    them (``sink.takes_tails``), else dense (the tails expanded into ``view``)."""
+    if tails is not None and getattr(sink, "takes_tails", False):
+        return sink(i0, i1, view, tails)
+    if tails is not None:
+        eng.expand(view, tails, i0, i1)
+    return sink(i0, i1, view)
+
+
 class RayEngine:
     """The basic state on one GPU and the fused RK45 kernels that read it."""
+
+    # constant row tails (rwrt_rk45_run_tails): frozen rays' rows are stored
+    # once per launch and expanded only for sinks that want dense rows; False:
+    # every row written by the launch itself (rwrt_rk45_run; A/B and tests)
+    use_tails = os.environ.get("RWRT_TAILS", "1") != "0"
 
     def __init__(self, fields, lon, lat, device=None):
         """``fields``: the reference stack ``[nlon(+1), nlat, 18]`` (numpy or tensor);
@@ -364,21 +401,32 @@ class RayEngine:
             return 0, 16
         return n_best, q_best
 
-    def run(self, st, p, tbound, it_begin, it_end, out, order=None, n_heavy=0, rays_per_wave=16):
-        """Rows ``[it_begin, it_end)`` into ``out[nray, it_end-it_begin, 8]`` (async)."""
+    def run(self, st, p, tbound, it_begin, it_end, out, order=None, n_heavy=0, rays_per_wave=16, tails=None):
+        """Rows ``[it_begin, it_end)`` into ``out[nray, it_end-it_begin, 8]`` (async);
+        with ``tails`` (a ``Tails``) the frozen rays' constant rows go there instead."""
         lib = H.load()
         if n_heavy:
             self.ctx.set_latency_density(rays_per_wave)
         if self.bg is None:
-            fn, bg = lib.rwrt_rk45_run, H.dptr(self.packed)
+            fn, bg = (lib.rwrt_rk45_run if tails is None else lib.rwrt_rk45_run_tails), H.dptr(self.packed)
         else:
-            fn, bg = lib.rwrt_rk45_run_tv, ctypes_ref(self.bg)
-        H.check(fn(
-            self.ctx.handle, self.grid, bg, st["nray"], ctypes_ref(p), H.dptr(tbound, F64),
-            int(it_begin), int(it_end), H.dptr(order, torch.int64), int(n_heavy),
-            H.dptr(st["state"]),
-            H.dptr(st["count"]), H.dptr(st["nanrow"]), H.dptr(out, F64), H.dptr(self.work),
-            self._stream()))
+            fn, bg = (lib.rwrt_rk45_run_tv if tails is None else lib.rwrt_rk45_run_tv_tails), ctypes_ref(self.bg)
+        args = [self.ctx.handle, self.grid, bg, st["nray"], ctypes_ref(p), H.dptr(tbound, F64),
+                int(it_begin), int(it_end), H.dptr(order, torch.int64), int(n_heavy),
+                H.dptr(st["state"]), H.dptr(st["count"]), H.dptr(st["nanrow"]), H.dptr(out, F64)]
+        if tails is not None:
+            args += [H.dptr(tails.frm, torch.int32), H.dptr(tails.row, F64)]
+        H.check(fn(*args, H.dptr(self.work), self._stream()))
+
+    def tails(self, nray):
+        """A ``Tails`` for ``nray`` rays, or None when the engine writes dense rows."""
+        return Tails(nray, self.device) if self.use_tails else None
+
+    def expand(self, view, tails, i0, i1):
+        """The rows ``[i0, i1)`` of a tails launch made dense: ``view[nray, i1-i0, 8]``
+        receives every ray's tail (rwrt_expand_tails; async)."""
+        H.check(H.load().rwrt_expand_tails(view.shape[0], int(i0), int(i1), H.dptr(tails.frm, torch.int32),
+                                           H.dptr(tails.row, F64), H.dptr(view, F64), self._stream()))
 
     def integrate_rk4(self, y0, nt, tstep, cut_off=0.1, chunk=None, sink=None, out=None,
                       cut_rad=None, events=None, group=None):
@@ -489,7 +537,10 @@ class RayEngine:
         piece is ordered by all the work so far."""
         auto = isinstance(split, str) and split.split(":")[0] == "auto"
         spec = split.split(":", 1)[1] if auto and ":" in split else ""
-        return auto, ([int(x) for x in spec.split(",")] if spec else [cls.SPLIT_ROWS])
+        rows = [int(x) for x in spec.split(",")] if spec else [cls.SPLIT_ROWS]
+        if any(n <= 0 for n in rows):
+            raise ValueError(f"split {split!r}: every piece needs a positive row count")
+        return auto, rows
 
     @staticmethod
     def cut_bounds(i0, i1, rows):
@@ -551,6 +602,7 @@ class RayEngine:
             i0 = bounds[-1][1]
         rows_max = max([b - a for a, b in bounds] or [1])
         bufs = _row_buffers(out, nray, rows_max, self.device)
+        tbufs = [self.tails(nray) for _ in bufs]   # (alternating with the row buffers)
         order = None
         if prev_work is None or order_policy not in ("cost", "priority", "cell", "total"):
             order = self.live_first_order_of(st)
@@ -587,17 +639,20 @@ class RayEngine:
             if os.environ.get("RWRT_DEBUG_TEAM"):
                 print(f"launch rows [{i0}, {i1}): n_heavy {n_heavy} at {qpw} per wave", flush=True)
             prev_work = cnt.sum(1)
+            tails = tbufs[k % len(bufs)]
             if events is not None:
                 e0, e1, es = self._event_pair()
-                self.run(st, p, tb, i0, i1, view, order, n_heavy, qpw)
+                self.run(st, p, tb, i0, i1, view, order, n_heavy, qpw, tails)
                 e1.record(es)
                 events.append((e0, e1))
             else:
-                self.run(st, p, tb, i0, i1, view, order, n_heavy, qpw)
+                self.run(st, p, tb, i0, i1, view, order, n_heavy, qpw, tails)
             if auto_split and k < n_lead:
                 works = (works + [cnt.sum(1) - prev_work])[-2:]
             if sink is not None:
-                sink(i0, i1, view)
+                deliver(self, sink, i0, i1, view, tails)
+            elif tails is not None and out is not None:
+                self.expand(view, tails, i0, i1)   # (the caller reads its own buffer: dense rows)
             k += 1
         mx = int(st["nanrow"].max().item()) if nray else 0
         if group is not None:
@@ -739,7 +794,7 @@ MATH_KINDS = {"sin": 0, "cos": 1, "tan": 2, "pow": 3, "atan2": 4, "mod": 5, "sqr
               "div2_first": 23,
               "div2_second": 24, "nm_sin": 25, "nm_cos": 26, "nm_tan": 27, "nm_pow": 28,
               "nm_rcp14": 29, "k_sin": 30, "k_cos": 31, "k_tan": 32, "k_pow": 33,
-              "qdiv": 34, "qdiv_exact_range": 35}
+              "qdiv": 34, "qdiv_exact_range": 35, "jump_verdict_fast": 36, "jump_verdict_exact": 37}
 
 
 def selftest_math(name, x, y=None, device="cuda"):

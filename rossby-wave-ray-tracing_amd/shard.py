@@ -6,6 +6,10 @@ crosses ranks is setup and collection only:
 
 * ``broadcast_array`` -- rank 0's basic-state stack (or initial rays) to every
   rank (RCCL broadcast over xGMI; ~1 MB at 2.5 deg, ~91 MB per 0.25 deg level);
+* ``broadcast_levels`` -- a time-varying background (C5): rank 0's u, v
+  snapshots (read or synthesised there only, as bs.py:202-262 reads a file
+  once) broadcast in blocks, every rank building its packed levels on its own
+  GPU (rwrt_bs_ready): 8.3 MB per 0.25-degree level instead of 100 MB packed;
 * ``shard_indices``   -- a balanced split: live rays and NaN-root slots are
   dealt round-robin separately, so every rank gets the same number of rays
   that actually integrate;
@@ -23,6 +27,8 @@ crosses ranks is setup and collection only:
 Works with the ``nccl`` (RCCL) backend on device tensors and with ``gloo`` on
 CPU tensors (tests/test_shard.py).
 """
+import time
+
 import numpy as np
 import torch
 import torch.distributed as dist
@@ -69,6 +75,37 @@ def broadcast_array(arr, src=0, group=None):
         t = torch.empty(shape, dtype=dtype, device=dev)
     dist.broadcast(t, src, group=group)
     return t.cpu().numpy()
+
+
+def broadcast_levels(lv, make_uv, group=None, src=0, block=16):
+    """Fill ``lv`` (a ``levels.Levels``, one per rank) with the same levels on
+    every rank: ``make_uv(j) -> (u, v)`` (float32 ``[nlat, nlon]``, file
+    layout) is called on rank ``src`` only; the snapshots travel in blocks of
+    ``block`` levels (RCCL broadcast of device tensors, or gloo on CPU
+    tensors) and each rank builds its packed records with ``rwrt_bs_ready``.
+    Returns ``{"levels", "bytes", "seconds", "collectives"}`` (bytes = what the
+    broadcasts carried; 0 collectives on one rank)."""
+    rank, world = world_info(group)
+    dev = _dev(group) if world > 1 else lv.device
+    t0 = time.perf_counter()
+    nbytes = ncoll = 0
+    for j0 in range(0, lv.nlev, block):
+        j1 = min(j0 + block, lv.nlev)
+        buf = torch.empty((j1 - j0, 2, lv.nlat, lv.nlon), dtype=torch.float32, device=dev)
+        if rank == src:
+            for j in range(j0, j1):
+                u, v = make_uv(j)
+                buf[j - j0, 0].copy_(torch.as_tensor(np.ascontiguousarray(u, np.float32)))
+                buf[j - j0, 1].copy_(torch.as_tensor(np.ascontiguousarray(v, np.float32)))
+        if world > 1:
+            dist.broadcast(buf, src, group=group)
+            nbytes += buf.numel() * buf.element_size()
+            ncoll += 1
+        for j in range(j0, j1):
+            lv.set_level(j, buf[j - j0, 0], buf[j - j0, 1])
+    torch.cuda.synchronize(lv.device)
+    return {"levels": int(lv.nlev), "bytes": int(nbytes), "seconds": time.perf_counter() - t0,
+            "collectives": ncoll}
 
 
 def reduce_summary(summary, group=None):
@@ -237,9 +274,10 @@ def run_sharded(eng, y0, nt, tstep=7200.0, group=None, rank=None, world=None, pr
         return ShardedRun(None, None, 0, failed=True)
     npr = min(probe, nt - 1)
     prow = torch.empty((nray, npr, 8), dtype=torch.float64, device=eng.device)
+    ptails = eng.tails(nray)
     if events is not None:
         e0, e1, es = eng._event_pair()
-    eng.run(st, p, tb, 1, 1 + npr, prow, eng.live_first_order_of(st), 0)
+    eng.run(st, p, tb, 1, 1 + npr, prow, eng.live_first_order_of(st), 0, tails=ptails)
     if events is not None:
         e1.record(es)
         events.append((e0, e1))
@@ -249,12 +287,20 @@ def run_sharded(eng, y0, nt, tstep=7200.0, group=None, rank=None, world=None, pr
     local = eng.take(st, idx)
     last = {}
 
-    def keep(i0, i1, rows):
-        last["row"] = rows[:, -1]
-        if sink is not None:
+    def keep(i0, i1, rows, tails=None):
+        # the endpoints need each ray's last row only: a frozen ray's is its tail
+        last["row"] = rows[:, -1] if tails is None else tails.last_row(rows, i1)
+        if sink is None:
+            return
+        if tails is not None and getattr(sink, "takes_tails", False):
+            sink(i0, i1, rows, idx, tails)
+        else:
+            if tails is not None:
+                eng.expand(rows, tails, i0, i1)   # (a sink that wants the rows dense)
             sink(i0, i1, rows, idx)
+    keep.takes_tails = True
 
-    keep(1, 1 + npr, prow[idx])
+    keep(1, 1 + npr, prow[idx], None if ptails is None else ptails.take(idx))
     n_live_local = int((~frozen[idx]).sum().item())
     res = eng.advance(local, p, tb, 1 + npr, chunk=chunk, sink=keep, out=out, events=events,
                       group=group, order_policy=order_policy, first_chunk=list(lead),

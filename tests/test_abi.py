@@ -56,7 +56,18 @@ def test_selftest_kinds_retired_are_errors():
         assert b"retired" in lib.rwrt_last_error()
     for kind in (0, 12, 16, 23, 35):
         assert lib.rwrt_selftest_math(kind, 0, None, None, None, None) == H.RWRT_OK
-    assert lib.rwrt_selftest_math(36, 0, None, None, None, None) == H.RWRT_ERR_ARG
+    assert lib.rwrt_selftest_math(38, 0, None, None, None, None) == H.RWRT_ERR_ARG
+    assert lib.rwrt_selftest_math(36, 0, None, None, None, None) == H.RWRT_OK   # (jump verdicts, round 5)
+
+
+def test_expand_tails_argument_errors():
+    """rwrt_expand_tails (ABI 3) validates before touching the device."""
+    lib = H.load()
+    assert lib.rwrt_expand_tails(-1, 1, 5, None, None, None, None) == H.RWRT_ERR_ARG
+    assert lib.rwrt_expand_tails(16, 5, 5, None, None, None, None) == H.RWRT_ERR_ARG
+    assert lib.rwrt_expand_tails(16, 1, 5, None, None, None, None) == H.RWRT_ERR_ARG
+    assert b"NULL" in lib.rwrt_last_error()
+    assert lib.rwrt_expand_tails(0, 1, 5, None, None, None, None) == H.RWRT_OK
 
 
 def test_context_needs_a_device():

@@ -78,3 +78,96 @@ def test_c5_10d_41_levels_bitwise_with_oracle(storage):
     assert np.array_equal(counts[:, 1], g["nrej"])
     # the sample crosses the level pairs: rays move, many still alive at 10 d
     assert np.nanmax(np.abs(hist[0, -1] - hist[0, 0])) > 0.5
+
+
+# ------------------------------------------------- C5 over a world-2 group
+def _c5_worker(rank, world, port, storage, q):
+    import os
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    sys.path[:0] = [os.path.join(root, "rossby-wave-ray-tracing_amd"), root, here, os.path.join(here, "golden")]
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import synthetic as S
+        from engine import RayEngine
+        from levels import Levels
+        from shard import broadcast_levels, gather_rows, run_sharded
+        g = np.load(os.path.join(here, "golden", f"c5_ref10_{storage}.npz"))
+        nt, nlev = int(g["nt"]), int(g["nlev"])
+        b0 = S.background_level(0, res=0.25)
+        lv = Levels(b0["lat"], b0["lon"], nlev, t0=0.0, dt=6 * 3600.0, fp32=storage == "fp32")
+        calls = []
+
+        def make_uv(j):   # called on rank 0 only
+            calls.append(j)
+            b = S.background_level(j, res=0.25)
+            return b["u"], b["v"]
+        info = broadcast_levels(lv, make_uv, group=dist.group.WORLD)
+        eng = RayEngine.from_levels(lv)
+        cfg = S.config("C5")
+        deg2rad = np.pi / 180.0
+        ix, iy = np.meshgrid(np.arange(cfg.nnx), np.arange(cfg.nny))
+        lon = ((cfg.SW_lon % 360.0 + ix.ravel() * cfg.dlon) % 360.0) * deg2rad
+        lat = (cfg.SW_lat + iy.ravel() * cfg.dlat) * deg2rad
+        src = eng.sources(lon, lat)
+        rows0 = torch.cat([eng.initial_rows_dev(src, eng.zwn_tensor(cfg.zwn, S.c3_freq(P)))[0].reshape(7, -1)
+                           for P in S.C3_PERIODS_DAYS], dim=1)
+        r0 = rows0[:, torch.as_tensor(g["idx"], device=eng.device)]
+        parts = []
+        r = run_sharded(eng, r0[:5].contiguous(), nt, 7200.0, group=dist.group.WORLD, probe=6, lead=[24, 96],
+                        chunk=48 if storage == "fp64" else 240, ttotal=(nt - 1) * 7200.0, order_policy="cell",
+                        sink=lambda a, b, o, idx: parts.append(o[:, :, :7].cpu()))
+        mine = torch.cat(parts, dim=1)                                   # (n_local, nt-1, 7)
+        full = gather_rows(mine, r.idx.cpu().numpy(), r0.shape[1], group=dist.group.WORLD)
+        if rank == 0:
+            q.put(("ok", full.numpy(), r0.cpu().numpy(), r.counts.cpu().numpy(), int(r.idx.numel()), info,
+                   len(calls)))
+        else:
+            q.put(("rank1", int(r.idx.numel()), info, len(calls)))
+    except Exception as e:  # pragma: no cover
+        q.put(("err", repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("storage", ["fp64", "fp32"])
+def test_c5_world2_split_bitwise_with_oracle(storage):
+    """BASELINE configs[4] split over a world-2 group (gloo; both ranks on this
+    GPU): rank 0 alone synthesises the 41 levels' u, v, which reach rank 1
+    through shard.broadcast_levels; the fixture's 4 096 rays are split by
+    measured cost (shard.run_sharded) and every rank's rows, gathered to rank
+    0, must hash like the oracle's in every row, with every ray's counts."""
+    import socket
+    import torch.multiprocessing as mp
+    g = golden(f"c5_ref10_{storage}.npz")
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_c5_worker, args=(r, 2, port, storage, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    msgs = [q.get(timeout=240) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+    ok = [m for m in msgs if m[0] == "ok"]
+    assert ok, msgs
+    _, full, r0, counts, n0, info0, calls0 = ok[0]
+    _, n1, info1, calls1 = [m for m in msgs if m[0] == "rank1"][0]
+    nt, nlev = int(g["nt"]), int(g["nlev"])
+    assert calls0 == nlev and calls1 == 0                       # only rank 0 made the snapshots
+    assert info1["bytes"] == nlev * 2 * 721 * 1440 * 4 and info1["collectives"] >= 1
+    assert n0 + n1 == r0.shape[1] and n0 > 0 and n1 > 0
+    hist = np.full((7, nt, r0.shape[1]), np.nan)
+    hist[:, 0] = r0
+    hist[:, 1:] = np.transpose(full, (2, 1, 0))
+    got = row_hashes(hist)
+    assert np.array_equal(got, g["row_sha"]), f"{int((got != g['row_sha']).sum())} of {nt} rows differ"
+    assert np.array_equal(counts[:, 0], g["nacc"])
+    assert np.array_equal(counts[:, 1], g["nrej"])

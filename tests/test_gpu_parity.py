@@ -363,6 +363,44 @@ def test_device_math_exactness():
     assert np.array_equal(selftest_math("floor_i32", fx), want)
 
 
+
+@pytest.mark.gpu
+def test_jump_verdict_fast_path_near_threshold():
+    """The jump mask's polynomial "no jump" shortcut (no_jump_fast, used by
+    cal_dis_reaches and quad_dis_reaches) gives the exact path's verdict on
+    steps straddling the threshold: with cut_off = 0.05 rad the
+    threshold lies inside the shortcut's |x| <= 1/16 window, which the bench's
+    0.1 rad x 2 h never reaches.  Steps of every direction are scaled so the
+    haversine distance (NumPy, wr.py:97-112) is cut_off (1 + eps) for eps from
+    -1e-3 to 1e-3 down to 1e-15 and exactly at the threshold."""
+    from engine import selftest_math
+    rng = np.random.default_rng(36)
+    lat_p, lon_p, cut = 0.6, 1.0, 0.05
+
+    def dist(dlat, dlon):
+        lat_c, lon_c = lat_p + dlat, lon_p + dlon
+        a = np.sin((lat_c - lat_p) / 2.0) ** 2 + (np.cos(lat_p) * np.cos(lat_c)) * np.sin((lon_c - lon_p) / 2.0) ** 2
+        return np.abs(2.0 * np.arctan2(np.sqrt(a), np.sqrt(1.0 - a)))
+
+    th = rng.uniform(0, 2 * np.pi, 512)
+    u, v = np.cos(th), np.sin(th) / np.cos(lat_p)
+    lo, hi = np.zeros_like(th), np.full_like(th, 0.2)
+    for _ in range(200):                       # bisect the scale to the threshold
+        mid = 0.5 * (lo + hi)
+        far = dist(mid * u, mid * v) >= cut
+        hi, lo = np.where(far, mid, hi), np.where(far, lo, mid)
+    eps = np.concatenate([-np.logspace(-3, -15, 25), [0.0], np.logspace(-15, -3, 25)])
+    s = (hi[:, None] * (1.0 + eps[None, :])).ravel()
+    dlat, dlon = s * np.repeat(u, eps.size), s * np.repeat(v, eps.size)
+    dlat = np.concatenate([dlat, np.nextafter(dlat, 0), np.nextafter(dlat, 1)])
+    dlon = np.concatenate([dlon, dlon, dlon])
+    fast = selftest_math("jump_verdict_fast", dlat, dlon)
+    exact = selftest_math("jump_verdict_exact", dlat, dlon)
+    assert np.array_equal(fast, exact)
+    assert 0.3 < exact.mean() < 0.7            # both verdicts occur
+    assert (np.abs(dlat / 2) <= 1 / 16).all() and (np.abs(dlon / 2) <= 1 / 16).all()   # inside the window
+
+
 # ------------------------------------------------------------------- RK4 mode
 def run_wr(kind, cfg_name, nt, inte_method):
     from wr import WR

@@ -2,6 +2,7 @@
 cell-ordered queue (C5), the rank correlation behind the adaptive split of
 the long launch, and the order they produce."""
 import numpy as np
+import pytest
 import torch
 
 import _hip as H
@@ -64,3 +65,6 @@ def test_long_launch_cuts():
     assert E.cut_bounds(189, 1081, [300, 300]) == [(189, 489), (489, 789), (789, 1081)]
     assert E.cut_bounds(189, 1081, [40]) == [(189, 229), (229, 1081)]
     assert E.cut_bounds(0, 100, [60, 60]) == [(0, 60), (60, 100)]        # a cut past the end is dropped
+    for bad in ("auto:0", "auto:-5", "auto:300,0"):                     # (empty / backward pieces)
+        with pytest.raises(ValueError):
+            E.parse_split(bad)

@@ -1,6 +1,12 @@
 """C4 on one MI355X: every rank's shard of the cost-balanced split, timed alone.
 
     python tools/c4_rehearsal.py [--days 90] [--worlds 1,2,4,8] [--out f.json]
+    python tools/c4_rehearsal.py --config C5 --fields fp64|fp32 [...]
+
+``--config C5`` splits BASELINE configs[4] instead (bench.py --config C5: the
+0.25-degree time-varying background, 361 levels, 9.67 M slots / 4.03 M live
+rays, the cell-ordered queue, 48-row launches for fp64 levels and 240 for
+fp32), the way ``bench.py --config C5 --gpus W`` splits it.
 
 For each world size W the C3 set is split exactly as ``bench.py --gpus W``
 splits it (shard.run_sharded: probe launch over every ray, snake deal by probe
@@ -38,6 +44,29 @@ def timed(fn, reps=2):
     return best, r
 
 
+def c5_setup(a, nt):
+    """bench.main_c5's engine and initial rays (one GPU, all 361 levels)."""
+    import synthetic as S
+    from levels import Levels
+    res, dt_bg = 0.25, 6 * 3600.0
+    nlev = int(np.ceil((nt - 1) * 7200.0 / dt_bg)) + 1
+    b0 = S.background_level(0, res=res)
+    lv = Levels(b0["lat"], b0["lon"], nlev, t0=0.0, dt=dt_bg, fp32=(a.fields == "fp32"))
+    for j in range(nlev):
+        bj = b0 if j == 0 else S.background_level(j, res=res)
+        lv.set_level(j, bj["u"], bj["v"])
+    eng = RayEngine.from_levels(lv)
+    cfg = S.config("C5")
+    deg2rad = np.pi / 180.0
+    ix, iy = np.meshgrid(np.arange(cfg.nnx), np.arange(cfg.nny))
+    lon = ((cfg.SW_lon % 360.0 + ix.ravel() * cfg.dlon) % 360.0) * deg2rad
+    lat = (cfg.SW_lat + iy.ravel() * cfg.dlat) * deg2rad
+    src = eng.sources(lon, lat)
+    y0 = torch.cat([eng.initial_rows_dev(src, eng.zwn_tensor(cfg.zwn, S.c3_freq(P)))[0][:5].reshape(5, -1)
+                    for P in S.C3_PERIODS_DAYS], dim=1)
+    return eng, y0.contiguous(), (240 if lv.fp32 else 48)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--days", type=float, default=90)
@@ -46,23 +75,34 @@ def main():
     ap.add_argument("--bg", default="zonal", choices=["zonal", "nonzonal"])
     ap.add_argument("--team", default="auto", help="latency-mode rays per launch (int or 'auto')")
     ap.add_argument("--lead", default="24,96", help="rows of the re-ordering launches after the probe (bench.py default for N > 1)")
+    ap.add_argument("--config", default="C3", choices=["C3", "C5"])
+    ap.add_argument("--fields", default="fp64", choices=["fp64", "fp32"], help="C5: level storage")
+    ap.add_argument("--reps", type=int, default=2)
     a = ap.parse_args()
     # 'auto', an int (rays per launch at 16 per wave) or n:q (n rays at q per wave)
     team = a.team if a.team == "auto" else (tuple(int(x) for x in a.team.split(":")) if ":" in a.team
                                              else int(a.team))
     lead = [int(x) for x in a.lead.split(",") if x]
-    bs, bg = bench.make_bs(a.bg)
-    y0 = torch.as_tensor(bench.c3_initial_state(bs), device="cuda")
-    eng = RayEngine.from_bs(bs)
     nt = int(a.days * 12) + 1
-    out = {"days": a.days, "bg": a.bg, "team": a.team, "lead": a.lead, "worlds": {}}
+    kw = {}
+    if a.config == "C5":
+        eng, y0, chunk = c5_setup(a, nt)
+        kw = dict(chunk=chunk, order_policy="cell", ttotal=(nt - 1) * 7200.0)
+        team = 0
+    else:
+        bs, bg = bench.make_bs(a.bg)
+        y0 = torch.as_tensor(bench.c3_initial_state(bs), device="cuda")
+        eng = RayEngine.from_bs(bs)
+    out = {"config": a.config, "days": a.days, "bg": a.bg if a.config == "C3" else "C5 time-varying",
+           "fields": a.fields if a.config == "C5" else "fp64", "team": a.team, "lead": a.lead,
+           "nslot": int(y0.shape[1]), "live": int((~torch.isnan(y0.sum(0))).sum().item()), "worlds": {}}
     for w in [int(x) for x in a.worlds.split(",")]:
         ranks = []
         for r in range(w):
             dt, res = timed(lambda: run_sharded(eng, y0, nt, rank=r, world=w, gather=False,
-                                                       team=team, lead=lead))
+                                                       team=team, lead=lead, **kw), reps=a.reps)
             ev = []
-            run_sharded(eng, y0, nt, rank=r, world=w, gather=False, team=team, lead=lead, events=ev)
+            run_sharded(eng, y0, nt, rank=r, world=w, gather=False, team=team, lead=lead, events=ev, **kw)
             torch.cuda.synchronize()
             launches = [dict(d, ms=a_.elapsed_time(b_)) for d, (a_, b_) in
                         zip([{"rows": [1, 1 + 6], "n_heavy": 0, "per_wave": 16}] + list(eng.launch_log), ev)]
@@ -75,6 +115,17 @@ def main():
         mk = max(x["s"] for x in ranks)
         out["worlds"][str(w)] = {"makespan_s": mk, "rate": steps / mk, "ray_steps": steps, "ranks": ranks}
         print(json.dumps({"world": w, "makespan_s": mk, "rate": steps / mk}), flush=True)
+    one1 = out["worlds"].get("1")
+    if one1:
+        for k, v in out["worlds"].items():
+            v["speedup_vs_1"] = one1["makespan_s"] / v["makespan_s"]
+            v["makespan_frac_of_1"] = v["makespan_s"] / one1["makespan_s"]
+    if a.config == "C5":
+        js = json.dumps(out)
+        print(js)
+        if a.out:
+            open(a.out, "w").write(js + "\n")
+        return
     # the heaviest ray alone (its attempts from the 1-rank run)
     full = run_sharded(eng, y0, nt, rank=0, world=1, gather=False)
     work = (full.res.nacc + full.res.nrej)
@@ -89,10 +140,6 @@ def main():
     out["attempts_per_live_ray"] = {"mean": float(w.mean()), "max": int(w.max()),
                                     "quantiles": dict(zip(["p50", "p90", "p99", "p999", "p9999"],
                                                           [float(x) for x in torch.quantile(w, q)]))}
-    one1 = out["worlds"].get("1")
-    if one1:
-        for k, v in out["worlds"].items():
-            v["speedup_vs_1"] = one1["makespan_s"] / v["makespan_s"]
     js = json.dumps(out)
     print(js)
     if a.out:
