@@ -523,7 +523,7 @@ class RayEngine:
     # correlates weakly (rank correlation below SPLIT_RHO: the non-zonal C3,
     # ~0.5, against ~0.8 on the zonal jets), the rest is split once after
     # SPLIT_ROWS rows and re-ordered by the work so far there
-    # (tools/c3_predictors.py, profiles/r3/sched/: the non-zonal last launch
+    # (round 3, profiles/r3/sched/: the non-zonal last launch
     # runs 1.66x its throughput bound in the predicted order, 1.00x in the
     # actual one; one split: +5 %).
     SPLIT_RHO = 0.7
