@@ -39,6 +39,13 @@ __device__ __forceinline__ bool rwrt_rare_sink(bool c) {
 #else
 #define RARE(c) (c)
 #endif
+// MARK(name): a named point in the analysis build's assembly (tools/hot_count.py
+// --marks counts the instructions between consecutive marks); nothing otherwise
+#ifdef RWRT_ANALYZE_MARK
+#define MARK(name) do { __builtin_amdgcn_sched_barrier(0); asm volatile("; @MARK " name); __builtin_amdgcn_sched_barrier(0); } while (0)
+#else
+#define MARK(name)
+#endif
 
 namespace rwrt {
 
@@ -2179,18 +2186,24 @@ __device__ __forceinline__ void quad_lookup_end(const CachedStaticBG& B, const Q
 // dy[4] (rB); aux as in ray_rhs (every lane).
 __device__ __forceinline__ void quad_rhs(const CachedStaticBG& B, const QuadRole& R, const double* y,
                                          double& rA, double& rB, double* aux) {
+  MARK("rhs");
   const double lon = y[0], lat = y[1], kx = y[2];
   const bool bad = fabs(lat) >= kHalfPi || fabs(y[3]) >= 100.0;
   const double ky = bad ? kNaN : y[3], amp = y[4];
   double g[11];
   const auto trig = np_math::nm_sincostan_begin(lat);
+  MARK("trig_begin_done");
   const KapTerms kw = kap_terms(kx, ky);
+  MARK("kap_done");
   const int rb = R.high ? R.role : R.role + 4;
   const auto pending = B.quad_begin(lon, lat, (unsigned)R.role * 1024u, (unsigned)(rb - 1) * 1024u);
+  MARK("cell_done");
   double s, c, tn;
   np_math::nm_sincostan_end(lat, trig, s, c, tn);
+  MARK("trig_end_done");
   __builtin_amdgcn_sched_barrier(0);
   quad_lookup_end(B, R, pending, g);
+  MARK("lookup_done");
   // Mercator (bs.py:856-883): M.cp == c off the pole band; there every
   // output takes mercator12_masked's extra factor m
   const Merc M = merc_factors(lat, c, s);
@@ -2207,6 +2220,7 @@ __device__ __forceinline__ void quad_rhs(const CachedStaticBG& B, const QuadRole
   const double fmqyy = mk ? (((g[F_QYY] * cp) - (g[F_QY] * M.s)) * cp) * m
                           : ((g[F_QYY] * cp) - (g[F_QY] * M.s)) * cp;
   const double kap = kw.kap, kap2 = kw.kap2;
+  MARK("merc_done");
   // slot 1: the quotients that need no other quotient
   double q1, q2;
   {
@@ -2222,6 +2236,7 @@ __device__ __forceinline__ void quad_rhs(const CachedStaticBG& B, const QuadRole
   const double ug = fmu + qu, vg = fmv + qv;                       // cal_ugvg (wn.py:266-294)
   const double dzwn = (-kx) * ((fmux + kap * fmvx) + qk);          // core_diffun (wr.py:53-78)
   const double dmwn = (-kx) * ((fmuy + kap * fmvy) + ql);
+  MARK("slot1_done");
   // slot 2
   double p1, p2;
   {
@@ -2241,6 +2256,7 @@ __device__ __forceinline__ void quad_rhs(const CachedStaticBG& B, const QuadRole
   aux[0] = ug;
   aux[1] = vg;
   aux[2] = bad ? kNaN : c;
+  MARK("slot2_done");
 }
 
 // The stage values K1..K5 this lane owns (variables `role` and 4), in its
@@ -2300,6 +2316,7 @@ __device__ __forceinline__ double quad_attempt(const CachedStaticBG& B, const Qu
       default: quad_epart(K, fA, fB, pA, pB); break;
     }
     (void)cn;   // (autonomous RHS: stage times unused)
+    MARK("stage_part_done");
     quad_rhs(B, R, ys, rA, rB, aux);
     if (s < 6) {
       K.put(s, rA, rB);
@@ -2312,6 +2329,7 @@ __device__ __forceinline__ double quad_attempt(const CachedStaticBG& B, const Qu
       ys[4] = ysB;
     }
   }
+  MARK("stages_done");
   // ys = y_new, (rA, rB) = K6; error estimate of the owned variables
 #pragma unroll
   for (int v = 0; v < 5; ++v) ynew[v] = ys[v];
@@ -2331,6 +2349,7 @@ __device__ __forceinline__ double quad_attempt(const CachedStaticBG& B, const Qu
   ss = ss + x2 * x2;
   ss = ss + x3 * x3;
   ss = ss + xB * xB;
+  MARK("error_norm_done");
   return sqrt(ss) / RootN<5>::v;
 }
 
@@ -3268,6 +3287,7 @@ struct rwrt_ctx {
   hipEvent_t flagged = nullptr, filled = nullptr;
   hipEvent_t done = nullptr;   // end of the last call on this context
   int quad_per_wave = 16;      // latency mode: rays per wave (rwrt_ctx_set_latency_density)
+  int reserved_cus = 0;        // CUs the persistent grid leaves free (rwrt_ctx_set_reserved_cus)
   int64_t* trace = nullptr;    // rwrt_ctx_set_trace (diagnostic)
   int64_t trace_cap = 0;
   bool used = false;
@@ -3398,6 +3418,7 @@ rwrt_status launch_run(rwrt_ctx* ctx, const BG& B, int64_t nray, const rwrt_para
   // latency-mode grid and launching it
   std::lock_guard<std::mutex> lock(ctx->mu);
   const int32_t quad_per_wave = ctx->quad_per_wave;
+  const int64_t reserved = ctx->reserved_cus;
   const int64_t per_block = 4 * (int64_t)quad_per_wave;   // rays per latency-mode block
   const int64_t team_blocks = (n_heavy + per_block - 1) / per_block;
   if (team_blocks > ctx->ncu / 2)
@@ -3410,7 +3431,8 @@ rwrt_status launch_run(rwrt_ctx* ctx, const BG& B, int64_t nray, const rwrt_para
   int64_t blocks = ctx_persistent_blocks<BG>(ctx);
   // latency-mode blocks take a CU each (their LDS does not fit beside a
   // persistent block): the persistent grid shrinks by as many CUs
-  if (team_blocks) blocks = std::max<int64_t>(1, blocks - team_blocks * (blocks / ctx->ncu));
+  // (and CUs reserved for a concurrent call on another context: rwrt_ctx_set_reserved_cus)
+  if (team_blocks + reserved) blocks = std::max<int64_t>(1, blocks - (team_blocks + reserved) * (blocks / ctx->ncu));
   const int64_t need = (nray - n_heavy + 255) / 256;
   if (blocks > need) blocks = need;
   RunArgs<BG> a{B, nray, p->rtol, p->atol, p->min_step, p->cut_off, p->nt, it_begin, it_end,
@@ -3642,6 +3664,14 @@ rwrt_status rwrt_ctx_set_latency_density(rwrt_ctx* c, int32_t rays_per_wave) {
   if (rays_per_wave < 1 || rays_per_wave > 16) return fail(RWRT_ERR_ARG, "rays_per_wave must be 1..16%s");
   std::lock_guard<std::mutex> lock(c->mu);
   c->quad_per_wave = rays_per_wave;
+  return RWRT_OK;
+}
+
+rwrt_status rwrt_ctx_set_reserved_cus(rwrt_ctx* c, int32_t cus) {
+  if (!c) return fail(RWRT_ERR_ARG, "rwrt_ctx is NULL%s");
+  if (cus < 0 || cus > c->ncu / 2) return fail(RWRT_ERR_ARG, "reserved CUs must be 0 .. half the device's CUs%s");
+  std::lock_guard<std::mutex> lock(c->mu);
+  c->reserved_cus = cus;
   return RWRT_OK;
 }
 

@@ -118,6 +118,17 @@ class RayEngine:
             self._ctx = H.Context(self.device)
         return self._ctx
 
+    _ctx_heavy = None
+
+    @property
+    def ctx_heavy(self):
+        """A second ``rwrt_ctx`` for a latency-mode call running beside this
+        engine's other calls on another stream (``shard.run_sharded``'s
+        ``heavy``): its own flags, side stream and events."""
+        if self._ctx_heavy is None:
+            self._ctx_heavy = H.Context(self.device)
+        return self._ctx_heavy
+
     def _stream(self):
         """The current stream of the engine's device (not torch's current device)."""
         return H.stream(self.device)
@@ -401,17 +412,20 @@ class RayEngine:
             return 0, 16
         return n_best, q_best
 
-    def run(self, st, p, tbound, it_begin, it_end, out, order=None, n_heavy=0, rays_per_wave=16, tails=None):
+    def run(self, st, p, tbound, it_begin, it_end, out, order=None, n_heavy=0, rays_per_wave=16, tails=None,
+            ctx=None):
         """Rows ``[it_begin, it_end)`` into ``out[nray, it_end-it_begin, 8]`` (async);
-        with ``tails`` (a ``Tails``) the frozen rays' constant rows go there instead."""
+        with ``tails`` (a ``Tails``) the frozen rays' constant rows go there instead.
+        ``ctx``: the context to run on (default: the engine's)."""
         lib = H.load()
+        ctx = ctx or self.ctx
         if n_heavy:
-            self.ctx.set_latency_density(rays_per_wave)
+            ctx.set_latency_density(rays_per_wave)
         if self.bg is None:
             fn, bg = (lib.rwrt_rk45_run if tails is None else lib.rwrt_rk45_run_tails), H.dptr(self.packed)
         else:
             fn, bg = (lib.rwrt_rk45_run_tv if tails is None else lib.rwrt_rk45_run_tv_tails), ctypes_ref(self.bg)
-        args = [self.ctx.handle, self.grid, bg, st["nray"], ctypes_ref(p), H.dptr(tbound, F64),
+        args = [ctx.handle, self.grid, bg, st["nray"], ctypes_ref(p), H.dptr(tbound, F64),
                 int(it_begin), int(it_end), H.dptr(order, torch.int64), int(n_heavy),
                 H.dptr(st["state"]), H.dptr(st["count"]), H.dptr(st["nanrow"]), H.dptr(out, F64)]
         if tails is not None:
