@@ -76,6 +76,29 @@ NM_FN double nm_copysign(double m, double s) {
 #define NM_LD(t, i) (t)[i]
 #endif
 #define tabd(t, i) nm_d(NM_LD(t, i))
+// The reads that always come in pairs or quadruples can be served together
+// (an includer storing the tables interleaved: one wide read each):
+//   NM_SINCOS4(k, sn, ssn, cs, ccs)  kG_SINCOSTAB[k .. k+3] (k a multiple of 4)
+//   NM_TAN2(j, hi, lo)               kT_TAN_HI[j], kT_TAN_LO[j]
+//   NM_KNOT2(k, a, n)                kRCP14_KNOT[k], kRCP14_KNOT[k+1] (k even)
+//   NM_LOG2(f, hi, lo), NM_EXP2(j, hi, lo)  kP_LOG_HI/LO[f], kP_EXP_HI/LO[j]
+#ifndef NM_SINCOS4
+#define NM_SINCOS4(k, a, b, c, d) \
+  (a = tabd(kG_SINCOSTAB, k), b = tabd(kG_SINCOSTAB, (k) + 1), c = tabd(kG_SINCOSTAB, (k) + 2), \
+   d = tabd(kG_SINCOSTAB, (k) + 3))
+#endif
+#ifndef NM_TAN2
+#define NM_TAN2(j, hi, lo) (hi = tabd(kT_TAN_HI, j), lo = tabd(kT_TAN_LO, j))
+#endif
+#ifndef NM_KNOT2
+#define NM_KNOT2(k, a, n) (a = NM_LD(kRCP14_KNOT, k), n = NM_LD(kRCP14_KNOT, (k) + 1))
+#endif
+#ifndef NM_LOG2
+#define NM_LOG2(f, hi, lo) (hi = tabd(kP_LOG_HI, f), lo = tabd(kP_LOG_LO, f))
+#endif
+#ifndef NM_EXP2
+#define NM_EXP2(j, hi, lo) (hi = tabd(kP_EXP_HI, j), lo = tabd(kP_EXP_LO, j))
+#endif
 // NM_ISSUE_FENCE(): the table reads above it are issued before the work below
 // (e.g. a scheduling barrier); nothing on the host
 #ifndef NM_ISSUE_FENCE
@@ -109,7 +132,9 @@ NM_FN double nm_rcp14_k(double x, unsigned A, unsigned N) {
 }
 NM_FN double nm_rcp14(double x) {
   const unsigned k = rcp14_knot(x);
-  return nm_rcp14_k(x, NM_LD(kRCP14_KNOT, k), NM_LD(kRCP14_KNOT, k + 1));
+  unsigned A, N;
+  NM_KNOT2(k, A, N);
+  return nm_rcp14_k(x, A, N);
 }
 
 // ---------------------------------------------------------------------------
@@ -136,8 +161,9 @@ struct GTab {
   double sn, ssn, cs, ccs;
 };
 NM_FN GTab g_tab(unsigned k) {
-  return GTab{tabd(kG_SINCOSTAB, k), tabd(kG_SINCOSTAB, k + 1), tabd(kG_SINCOSTAB, k + 2),
-              tabd(kG_SINCOSTAB, k + 3)};
+  GTab T;
+  NM_SINCOS4(k, T.sn, T.ssn, T.cs, T.ccs);
+  return T;
 }
 // do_sin(x, dx) with the table entry of x fetched by the caller (below 0.126
 // the Taylor branch's value is returned)
@@ -329,11 +355,15 @@ NM_FN double nm_tan_fin(const TanPre& t, unsigned A, unsigned Nk) {
 NM_FN double nm_tan_t(double x, double T, double Tl) {
   const TanPre t = nm_tan_pre(x, T, Tl);
   const unsigned k = rcp14_knot(t.D);
-  return nm_tan_fin(t, NM_LD(kRCP14_KNOT, k), NM_LD(kRCP14_KNOT, k + 1));
+  unsigned A, N;
+  NM_KNOT2(k, A, N);
+  return nm_tan_fin(t, A, N);
 }
 NM_FN double nm_tan_main(double x) {
   const int j = t_index(x);
-  return nm_tan_t(x, tabd(kT_TAN_HI, j), tabd(kT_TAN_LO, j));
+  double T, Tl;
+  NM_TAN2(j, T, Tl);
+  return nm_tan_t(x, T, Tl);
 }
 NM_FN double nm_tan(double x) {
   const double v = nm_tan_main(x);
@@ -348,12 +378,14 @@ NM_FN double nm_tan(double x) {
 //   reciprocal's knots | sin and cos | tan
 NM_FN void nm_sincostan(double x, double& sn, double& cs, double& tn) {
   const int j = t_index(x);
-  const double T = tabd(kT_TAN_HI, j), Tl = tabd(kT_TAN_LO, j);
+  double T, Tl;
+  NM_TAN2(j, T, Tl);
   const SinCosPre P = nm_sincos_tab(x);
   NM_ISSUE_FENCE();
   const TanPre tp = nm_tan_pre(x, T, Tl);
   const unsigned k = rcp14_knot(tp.D);
-  const unsigned A = NM_LD(kRCP14_KNOT, k), Nk = NM_LD(kRCP14_KNOT, k + 1);
+  unsigned A, Nk;
+  NM_KNOT2(k, A, Nk);
   NM_ISSUE_FENCE();
   nm_sincos_fin(x, P, sn, cs);
   tn = nm_tan_fin(tp, A, Nk);
@@ -375,13 +407,13 @@ struct SinCosTanPre {
 NM_FN SinCosTanPre nm_sincostan_begin(double x) {
   SinCosTanPre r;
   const int j = t_index(x);
-  const double T = tabd(kT_TAN_HI, j), Tl = tabd(kT_TAN_LO, j);
+  double T, Tl;
+  NM_TAN2(j, T, Tl);
   r.P = nm_sincos_tab(x);
   NM_ISSUE_FENCE();
   r.tp = nm_tan_pre(x, T, Tl);
   const unsigned k = rcp14_knot(r.tp.D);
-  r.A = NM_LD(kRCP14_KNOT, k);
-  r.Nk = NM_LD(kRCP14_KNOT, k + 1);
+  NM_KNOT2(k, r.A, r.Nk);
   return r;
 }
 NM_FN void nm_sincostan_end(double x, const SinCosTanPre& r, double& sn, double& cs, double& tn) {
@@ -450,7 +482,8 @@ NM_FN double nm_pow(double x, double y) {
   const int f = (int)((nm_u(R) >> 47) & 31);
   double e = (double)ex;
   if (R < 1.5) e = e + 1.0;
-  const double Lh = tabd(kP_LOG_HI, f), Ll = tabd(kP_LOG_LO, f);
+  double Lh, Ll;
+  NM_LOG2(f, Lh, Ll);
   const double r = nm_fma(m * nm_d(kP_HALF), R, -nm_d(kP_HALF));
   const double r2 = r * r;
   const double a9 = nm_fma(nm_d(kP_C10), r, nm_d(kP_C9));
@@ -498,7 +531,8 @@ NM_FN double nm_pow(double x, double y) {
   const double p5 = nm_fma(nm_d(kP_E2), fz, nm_d(kP_E1));
   p1 = nm_fma(f2, p1, p3);
   p1 = nm_fma(f2, p1, p5);
-  const double El = tabd(kP_EXP_LO, jj), Eh = tabd(kP_EXP_HI, jj);
+  double Eh, El;
+  NM_EXP2(jj, Eh, El);
   p1 = nm_fma(fz, p1, El);
   p1 = nm_fma(Eh, p1, Eh);
   const double scale = nm_d((unsigned long long)(kk + 1023) << 52);

@@ -1050,16 +1050,44 @@ __device__ __forceinline__ double add_rd(double a, double b) {
 // The tables live in LDS inside the kernels (staged at kernel entry by
 // nm_stage): per-lane table reads from global memory would share vmcnt with
 // the cell cache's LDS-DMA refills, so every read would also wait for the
-// refill the RHS issued before its trigonometry.
-__shared__ unsigned long long nm_lds_kG_SINCOSTAB[440];
-__shared__ unsigned long long nm_lds_kT_TAN_HI[16];
-__shared__ unsigned long long nm_lds_kT_TAN_LO[16];
-__shared__ unsigned long long nm_lds_kP_LOG_HI[32];
-__shared__ unsigned long long nm_lds_kP_LOG_LO[32];
-__shared__ unsigned long long nm_lds_kP_EXP_HI[16];
-__shared__ unsigned long long nm_lds_kP_EXP_LO[16];
-__shared__ unsigned nm_lds_kRCP14_KNOT[128];
-#define NM_LD(t, i) nm_lds_##t[i]
+// refill the RHS issued before its trigonometry.  Stored interleaved, so
+// that each pair of values read together is one 16-B read (one 8-B read for
+// the reciprocal's knots): the sin/cos table as two arrays of (sn, ssn) and
+// (cs, ccs) pairs -- a lane's pair j sits in 16-B bank slot j mod 16 of its
+// array, where the flat table put the pairs of the 64 lanes' lane-random
+// reads in 8 slots -- tan's, log's and exp's (head, tail) pairs, the knots'
+// (A, N) pairs.  Same values, so the same results.
+__shared__ __attribute__((aligned(16))) double2 nm_lds_sc_s[110];    // kG_SINCOSTAB[4j], [4j + 1]
+__shared__ __attribute__((aligned(16))) double2 nm_lds_sc_c[110];    // kG_SINCOSTAB[4j + 2], [4j + 3]
+__shared__ __attribute__((aligned(16))) double2 nm_lds_tan[16];      // kT_TAN_HI[j], kT_TAN_LO[j]
+__shared__ __attribute__((aligned(16))) double2 nm_lds_log[32];      // kP_LOG_HI[f], kP_LOG_LO[f]
+__shared__ __attribute__((aligned(16))) double2 nm_lds_exp[16];      // kP_EXP_HI[j], kP_EXP_LO[j]
+__shared__ __attribute__((aligned(8))) uint2 nm_lds_knot[64];        // kRCP14_KNOT[2i], [2i + 1]
+#define NM_SINCOS4(k, a, b, c, d)                        \
+  do {                                                   \
+    const double2 nm_s_ = nm_lds_sc_s[(k) >> 2];         \
+    const double2 nm_c_ = nm_lds_sc_c[(k) >> 2];         \
+    a = nm_s_.x;                                         \
+    b = nm_s_.y;                                         \
+    c = nm_c_.x;                                         \
+    d = nm_c_.y;                                         \
+  } while (0)
+#define NM_PAIR_(arr, i, hi, lo)       \
+  do {                                 \
+    const double2 nm_p_ = arr[i];      \
+    hi = nm_p_.x;                      \
+    lo = nm_p_.y;                      \
+  } while (0)
+#define NM_TAN2(j, hi, lo) NM_PAIR_(nm_lds_tan, j, hi, lo)
+#define NM_LOG2(f, hi, lo) NM_PAIR_(nm_lds_log, f, hi, lo)
+#define NM_EXP2(j, hi, lo) NM_PAIR_(nm_lds_exp, j, hi, lo)
+#define NM_KNOT2(k, a, n)                    \
+  do {                                       \
+    const uint2 nm_k_ = nm_lds_knot[(k) >> 1]; \
+    a = nm_k_.x;                             \
+    n = nm_k_.y;                             \
+  } while (0)
+#define NM_LD(t, i) NM_LD_unused_##t
 // (The polynomial constants stay s_mov_b32 pairs: as scalar loads they share
 // lgkmcnt with the LDS reads, 0.99x; from LDS the round trip lands on the
 // polynomial chains, 0.91x -- profiles/r2/ab/const_lds.txt.)
@@ -1074,24 +1102,21 @@ enum { NM_SINCOS = 1, NM_TAN = 2, NM_POW = 4, NM_ALL = 7 };
 template <int MASK>
 __device__ __forceinline__ void nm_stage() {
   const int t = threadIdx.x, nt = blockDim.x;
+  auto d = [](unsigned long long u) { return __builtin_bit_cast(double, u); };
   if (MASK & NM_SINCOS)
-    for (int i = t; i < 440; i += nt) nm_lds_kG_SINCOSTAB[i] = np_math::kG_SINCOSTAB[i];
-  if (MASK & NM_TAN)
-    for (int i = t; i < 16; i += nt) {
-      nm_lds_kT_TAN_HI[i] = np_math::kT_TAN_HI[i];
-      nm_lds_kT_TAN_LO[i] = np_math::kT_TAN_LO[i];
+    for (int i = t; i < 110; i += nt) {
+      nm_lds_sc_s[i] = make_double2(d(np_math::kG_SINCOSTAB[4 * i]), d(np_math::kG_SINCOSTAB[4 * i + 1]));
+      nm_lds_sc_c[i] = make_double2(d(np_math::kG_SINCOSTAB[4 * i + 2]), d(np_math::kG_SINCOSTAB[4 * i + 3]));
     }
+  if (MASK & NM_TAN)
+    for (int i = t; i < 16; i += nt) nm_lds_tan[i] = make_double2(d(np_math::kT_TAN_HI[i]), d(np_math::kT_TAN_LO[i]));
   if (MASK & NM_POW)
     for (int i = t; i < 32; i += nt) {
-      nm_lds_kP_LOG_HI[i] = np_math::kP_LOG_HI[i];
-      nm_lds_kP_LOG_LO[i] = np_math::kP_LOG_LO[i];
-      if (i < 16) {
-        nm_lds_kP_EXP_HI[i] = np_math::kP_EXP_HI[i];
-        nm_lds_kP_EXP_LO[i] = np_math::kP_EXP_LO[i];
-      }
+      nm_lds_log[i] = make_double2(d(np_math::kP_LOG_HI[i]), d(np_math::kP_LOG_LO[i]));
+      if (i < 16) nm_lds_exp[i] = make_double2(d(np_math::kP_EXP_HI[i]), d(np_math::kP_EXP_LO[i]));
     }
   if (MASK & (NM_TAN | NM_POW))
-    for (int i = t; i < 128; i += nt) nm_lds_kRCP14_KNOT[i] = np_math::kRCP14_KNOT[i];
+    for (int i = t; i < 64; i += nt) nm_lds_knot[i] = make_uint2(np_math::kRCP14_KNOT[2 * i], np_math::kRCP14_KNOT[2 * i + 1]);
   __syncthreads();
 }
 
@@ -2210,15 +2235,22 @@ __device__ __forceinline__ void quad_rhs(const CachedStaticBG& B, const QuadRole
   const double cp = M.cp, m = M.m;
   const bool mk = m != 1.0;
   const double fu = g[F_U], fv = g[F_V];
-  const double fmuy = mk ? (g[F_UY] + tn * fu) * m : g[F_UY] + tn * fu;
-  const double fmvy = mk ? (g[F_VY] + tn * fv) * m : g[F_VY] + tn * fv;
-  const double fmqx = mk ? g[F_QX] * m : g[F_QX];
-  const double fmqy = mk ? (g[F_QY] * cp) * m : g[F_QY] * cp;
-  const double fmqxx = mk ? g[F_QXX] * m : g[F_QXX];
-  const double fmqyx = mk ? (g[F_QXY] * cp) * m : g[F_QXY] * cp;
-  const double fmqxy = mk ? fmqyx * m : fmqyx;
-  const double fmqyy = mk ? (((g[F_QYY] * cp) - (g[F_QY] * M.s)) * cp) * m
-                          : ((g[F_QYY] * cp) - (g[F_QY] * M.s)) * cp;
+  // (the mask's factor on a branch, not as selects: 24 v_cndmask per RHS
+  // on the common path otherwise)
+  double fmuy = g[F_UY] + tn * fu, fmvy = g[F_VY] + tn * fv;
+  double fmqx = g[F_QX], fmqy = g[F_QY] * cp, fmqxx = g[F_QXX], fmqyx = g[F_QXY] * cp;
+  double fmqxy = fmqyx, fmqyy = ((g[F_QYY] * cp) - (g[F_QY] * M.s)) * cp;
+  if (RARE(mk)) {
+    asm volatile("");   // the pole band (rare branch)
+    fmuy = fmuy * m;
+    fmvy = fmvy * m;
+    fmqx = fmqx * m;
+    fmqy = fmqy * m;
+    fmqxx = fmqxx * m;
+    fmqyx = fmqyx * m;
+    fmqxy = fmqyx * m;
+    fmqyy = fmqyy * m;
+  }
   const double kap = kw.kap, kap2 = kw.kap2;
   MARK("merc_done");
   // slot 1: the quotients that need no other quotient
@@ -2231,8 +2263,14 @@ __device__ __forceinline__ void quad_rhs(const CachedStaticBG& B, const QuadRole
   }
   const double du = qbcast<0>(q1), dv = qbcast<0>(q2), dux = qbcast<1>(q1), dvx = qbcast<1>(q2);
   const double qu = qbcast<2>(q1), qv = qbcast<2>(q2), qk = qbcast<3>(q1), ql = qbcast<3>(q2);
-  const double fmu = mk ? du * m : du, fmv = mk ? dv * m : dv;
-  const double fmux = mk ? dux * m : dux, fmvx = mk ? dvx * m : dvx;
+  double fmu = du, fmv = dv, fmux = dux, fmvx = dvx;
+  if (RARE(mk)) {
+    asm volatile("");   // the pole band (rare branch)
+    fmu = du * m;
+    fmv = dv * m;
+    fmux = dux * m;
+    fmvx = dvx * m;
+  }
   const double ug = fmu + qu, vg = fmv + qv;                       // cal_ugvg (wn.py:266-294)
   const double dzwn = (-kx) * ((fmux + kap * fmvx) + qk);          // core_diffun (wr.py:53-78)
   const double dmwn = (-kx) * ((fmuy + kap * fmvy) + ql);

@@ -413,10 +413,12 @@ class RayEngine:
         return n_best, q_best
 
     def run(self, st, p, tbound, it_begin, it_end, out, order=None, n_heavy=0, rays_per_wave=16, tails=None,
-            ctx=None):
+            ctx=None, work=None):
         """Rows ``[it_begin, it_end)`` into ``out[nray, it_end-it_begin, 8]`` (async);
         with ``tails`` (a ``Tails``) the frozen rays' constant rows go there instead.
-        ``ctx``: the context to run on (default: the engine's)."""
+        ``ctx``: the context to run on (default: the engine's); ``work``: the
+        queue scratch (default: the engine's -- a call running concurrently
+        with another needs its own)."""
         lib = H.load()
         ctx = ctx or self.ctx
         if n_heavy:
@@ -430,7 +432,7 @@ class RayEngine:
                 H.dptr(st["state"]), H.dptr(st["count"]), H.dptr(st["nanrow"]), H.dptr(out, F64)]
         if tails is not None:
             args += [H.dptr(tails.frm, torch.int32), H.dptr(tails.row, F64)]
-        H.check(fn(*args, H.dptr(self.work), self._stream()))
+        H.check(fn(*args, H.dptr(self.work if work is None else work), self._stream()))
 
     def tails(self, nray):
         """A ``Tails`` for ``nray`` rays, or None when the engine writes dense rows."""

@@ -246,6 +246,7 @@ def _run_with_heavy(eng, local, idx, hv, p, tb, start, nt, keep, last, sink, chu
     k = int(hv.numel())
     cus = -(-k // 64)                                   # latency-mode blocks: 64 rays (16 per wave) per CU
     out_h = torch.empty((k, nt - start, 8), dtype=torch.float64, device=dev)
+    work_h = torch.zeros(4, dtype=torch.int32, device=dev)
     tails_h = eng.tails(k)
     cur = torch.cuda.current_stream(dev)
     side = torch.cuda.Stream(device=dev)
@@ -253,8 +254,9 @@ def _run_with_heavy(eng, local, idx, hv, p, tb, start, nt, keep, last, sink, chu
     ready.record(cur)
     with torch.cuda.stream(side):
         side.wait_event(ready)
+        # (its own queue scratch: the two calls run at the same time)
         eng.run(st_h, p, tb, start, nt, out_h, torch.arange(k, dtype=torch.int64, device=dev), k, 16,
-                tails=tails_h, ctx=eng.ctx_heavy)
+                tails=tails_h, ctx=eng.ctx_heavy, work=work_h)
         done = torch.cuda.Event()
         done.record(side)
     rest_last = {}

@@ -15,7 +15,7 @@ import json
 import sys
 
 
-KERNELS = ("rk45_run_kernel", "frozen_fill_kernel", "frozen_flag_kernel")
+KERNELS = ("rk45_run_kernel", "frozen_fill_kernel", "frozen_flag_kernel", "frozen_tail_kernel")
 
 
 def per_launch(d, counter):
@@ -27,6 +27,19 @@ def per_launch(d, counter):
             total += float(r["Counter_Value"]) * 1024.0
             launches += "rk45_run_kernel" in r["Kernel_Name"]
     return [total / max(launches, 1)] * launches
+
+
+def by_kernel(d, counter):
+    """Bytes per call of each of the call's kernels (run kernel dispatches = calls)."""
+    tot, launches = {}, 0
+    for r in csv.DictReader(open(f"{d}/run_counter_collection.csv")):
+        if r["Counter_Name"] != counter:
+            continue
+        k = next((k for k in KERNELS if k in r["Kernel_Name"]), None)
+        if k:
+            tot[k] = tot.get(k, 0.0) + float(r["Counter_Value"]) * 1024.0
+            launches += k == "rk45_run_kernel"
+    return {k: v / max(launches, 1) for k, v in tot.items()}
 
 
 def main():
@@ -47,6 +60,8 @@ def main():
            "kernel": "rk45_run_kernel", "kernels_summed": list(KERNELS), "launches": n,
            "fetch_bytes_per_launch_x2": 2 * fb, "write_bytes_per_launch": wb,
            "traffic_bytes_per_launch": 2 * fb + wb,
+           "write_bytes_per_launch_by_kernel": by_kernel(write_dir, "WRITE_SIZE"),
+           "fetch_bytes_per_launch_by_kernel_x2": {k: 2 * v for k, v in by_kernel(fetch_dir, "FETCH_SIZE").items()},
            "algorithmic_bytes_per_launch": steps_per_launch * bps,
            "note": "FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE; counters in KiB x 1024"}
     json.dump(res, open(out, "w"), indent=1)
