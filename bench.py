@@ -273,8 +273,6 @@ def schedule_defaults(args, world):
         args.probe = 4 if whole else 6
     if args.team is None:
         args.team = ("64,64,64" if args.bg == "zonal" else "0") if whole else "auto"
-    if args.heavy is None:
-        args.heavy = 0 if (whole or args.config != "C3") else 128
     return args
 
 
@@ -393,10 +391,6 @@ def main():
                          "an integer, one per launch after the probe (e.g. 64,256,64; the last "
                          "repeats) or 'auto' (RayEngine.team_size).  Default: 64,64,64 for a whole C3 "
                          "set per GPU, auto for a split one")
-    ap.add_argument("--heavy", type=int, default=None,
-                    help="rays per rank (by probe attempts) run over the whole rest of the horizon in ONE "
-                         "latency-mode call on a second stream beside the other rays' launches "
-                         "(shard.run_sharded heavy); default 128 for a split C3 set, 0 otherwise")
     ap.add_argument("--lib", default=None, help="alternative librwrt build (A/B timing)")
     ap.add_argument("--traffic", default=None, help="traffic.json (tools/pmc_traffic.py)")
     ap.add_argument("--valu-profile", default=None, help="valu.json (tools/pmc_valu.py)")
@@ -530,12 +524,12 @@ def main():
         if weak:
             r = run_sharded(eng, y, nt, 7200.0, rank=0, world=1, probe=args.probe, lead=lead,
                             chunk=chunk, out=out, events=events, ttotal=(nt - 1) * 7200.0,
-                            order_policy=args.order, team=team, split=split, heavy=args.heavy)
+                            order_policy=args.order, team=team, split=split)
             gather_endpoints(r)
             return r
         return run_sharded(eng, y, nt, 7200.0, group=group, probe=args.probe, lead=lead,
                            chunk=chunk, out=out, events=events, ttotal=(nt - 1) * 7200.0,
-                           order_policy=args.order, team=team, split=split, heavy=args.heavy)
+                           order_policy=args.order, team=team, split=split)
 
     for _ in range(args.warmup):
         one_step()
@@ -614,7 +608,6 @@ def main():
             "queue_order": args.order,
             "long_launch_split": {"mode": args.split, "rank_corr_of_leading_launches": eng.split_rho,
                                   "threshold": eng.SPLIT_RHO, "rows": eng.SPLIT_ROWS},
-            "heavy_stream": getattr(r.res, "heavy", None),
             "library": os.path.basename(os.environ.get("RWRT_LIB", "librwrt.so")),
             "library_sha256": library_sha(),
             "roofline": roofline(per_launch_steps, avg_launch_s, workload, schedule, BYTES_PER_STEP, args,

@@ -99,12 +99,6 @@ rwrt_status rwrt_ctx_destroy(rwrt_ctx* ctx);
  * other rays' cell refills and interval ends) at more CUs per heavy ray.
  * Schedule only: results do not depend on it. */
 rwrt_status rwrt_ctx_set_latency_density(rwrt_ctx* ctx, int32_t rays_per_wave);
-/* CUs (0 .. half the device's) that the persistent grid of this context's
- * rwrt_rk45_run calls leaves free (default 0), so that a call on ANOTHER
- * context and stream -- e.g. a latency-mode call over a few heavy rays
- * spanning many row windows -- holds its blocks beside them (ABI 3).
- * Schedule only: results do not depend on it. */
-rwrt_status rwrt_ctx_set_reserved_cus(rwrt_ctx* ctx, int32_t cus);
 /* Diagnostic ray trace of the context's rwrt_rk45_run calls (NULL / 0: off):
  * for queue positions w < capacity of the order, the ray's lane records
  * d_trace[w * 10 + 0..9] = {ray, hardware id (HW_REG_HW_ID: wave, SIMD, CU,

@@ -1057,6 +1057,10 @@ __device__ __forceinline__ double add_rd(double a, double b) {
 // array, where the flat table put the pairs of the 64 lanes' lane-random
 // reads in 8 slots -- tan's, log's and exp's (head, tail) pairs, the knots'
 // (A, N) pairs.  Same values, so the same results.
+#ifndef RWRT_NM_INTERLEAVED
+#define RWRT_NM_INTERLEAVED 1
+#endif
+#if RWRT_NM_INTERLEAVED
 __shared__ __attribute__((aligned(16))) double2 nm_lds_sc_s[110];    // kG_SINCOSTAB[4j], [4j + 1]
 __shared__ __attribute__((aligned(16))) double2 nm_lds_sc_c[110];    // kG_SINCOSTAB[4j + 2], [4j + 3]
 __shared__ __attribute__((aligned(16))) double2 nm_lds_tan[16];      // kT_TAN_HI[j], kT_TAN_LO[j]
@@ -1088,6 +1092,17 @@ __shared__ __attribute__((aligned(8))) uint2 nm_lds_knot[64];        // kRCP14_K
     n = nm_k_.y;                             \
   } while (0)
 #define NM_LD(t, i) NM_LD_unused_##t
+#else   // (round 4's flat tables: A/B)
+__shared__ unsigned long long nm_lds_kG_SINCOSTAB[440];
+__shared__ unsigned long long nm_lds_kT_TAN_HI[16];
+__shared__ unsigned long long nm_lds_kT_TAN_LO[16];
+__shared__ unsigned long long nm_lds_kP_LOG_HI[32];
+__shared__ unsigned long long nm_lds_kP_LOG_LO[32];
+__shared__ unsigned long long nm_lds_kP_EXP_HI[16];
+__shared__ unsigned long long nm_lds_kP_EXP_LO[16];
+__shared__ unsigned nm_lds_kRCP14_KNOT[128];
+#define NM_LD(t, i) nm_lds_##t[i]
+#endif
 // (The polynomial constants stay s_mov_b32 pairs: as scalar loads they share
 // lgkmcnt with the LDS reads, 0.99x; from LDS the round trip lands on the
 // polynomial chains, 0.91x -- profiles/r2/ab/const_lds.txt.)
@@ -1102,6 +1117,26 @@ enum { NM_SINCOS = 1, NM_TAN = 2, NM_POW = 4, NM_ALL = 7 };
 template <int MASK>
 __device__ __forceinline__ void nm_stage() {
   const int t = threadIdx.x, nt = blockDim.x;
+#if !RWRT_NM_INTERLEAVED
+  if (MASK & NM_SINCOS)
+    for (int i = t; i < 440; i += nt) nm_lds_kG_SINCOSTAB[i] = np_math::kG_SINCOSTAB[i];
+  if (MASK & NM_TAN)
+    for (int i = t; i < 16; i += nt) {
+      nm_lds_kT_TAN_HI[i] = np_math::kT_TAN_HI[i];
+      nm_lds_kT_TAN_LO[i] = np_math::kT_TAN_LO[i];
+    }
+  if (MASK & NM_POW)
+    for (int i = t; i < 32; i += nt) {
+      nm_lds_kP_LOG_HI[i] = np_math::kP_LOG_HI[i];
+      nm_lds_kP_LOG_LO[i] = np_math::kP_LOG_LO[i];
+      if (i < 16) {
+        nm_lds_kP_EXP_HI[i] = np_math::kP_EXP_HI[i];
+        nm_lds_kP_EXP_LO[i] = np_math::kP_EXP_LO[i];
+      }
+    }
+  if (MASK & (NM_TAN | NM_POW))
+    for (int i = t; i < 128; i += nt) nm_lds_kRCP14_KNOT[i] = np_math::kRCP14_KNOT[i];
+#else
   auto d = [](unsigned long long u) { return __builtin_bit_cast(double, u); };
   if (MASK & NM_SINCOS)
     for (int i = t; i < 110; i += nt) {
@@ -1117,6 +1152,7 @@ __device__ __forceinline__ void nm_stage() {
     }
   if (MASK & (NM_TAN | NM_POW))
     for (int i = t; i < 64; i += nt) nm_lds_knot[i] = make_uint2(np_math::kRCP14_KNOT[2 * i], np_math::kRCP14_KNOT[2 * i + 1]);
+#endif
   __syncthreads();
 }
 
@@ -2237,6 +2273,20 @@ __device__ __forceinline__ void quad_rhs(const CachedStaticBG& B, const QuadRole
   const double fu = g[F_U], fv = g[F_V];
   // (the mask's factor on a branch, not as selects: 24 v_cndmask per RHS
   // on the common path otherwise)
+#ifndef RWRT_QUAD_MASK_BRANCH
+#define RWRT_QUAD_MASK_BRANCH 1
+#endif
+#if !RWRT_QUAD_MASK_BRANCH   // (round 4: selects)
+  const double fmuy = mk ? (g[F_UY] + tn * fu) * m : g[F_UY] + tn * fu;
+  const double fmvy = mk ? (g[F_VY] + tn * fv) * m : g[F_VY] + tn * fv;
+  const double fmqx = mk ? g[F_QX] * m : g[F_QX];
+  const double fmqy = mk ? (g[F_QY] * cp) * m : g[F_QY] * cp;
+  const double fmqxx = mk ? g[F_QXX] * m : g[F_QXX];
+  const double fmqyx = mk ? (g[F_QXY] * cp) * m : g[F_QXY] * cp;
+  const double fmqxy = mk ? fmqyx * m : fmqyx;
+  const double fmqyy = mk ? (((g[F_QYY] * cp) - (g[F_QY] * M.s)) * cp) * m
+                          : ((g[F_QYY] * cp) - (g[F_QY] * M.s)) * cp;
+#else
   double fmuy = g[F_UY] + tn * fu, fmvy = g[F_VY] + tn * fv;
   double fmqx = g[F_QX], fmqy = g[F_QY] * cp, fmqxx = g[F_QXX], fmqyx = g[F_QXY] * cp;
   double fmqxy = fmqyx, fmqyy = ((g[F_QYY] * cp) - (g[F_QY] * M.s)) * cp;
@@ -2251,6 +2301,7 @@ __device__ __forceinline__ void quad_rhs(const CachedStaticBG& B, const QuadRole
     fmqxy = fmqyx * m;
     fmqyy = fmqyy * m;
   }
+#endif
   const double kap = kw.kap, kap2 = kw.kap2;
   MARK("merc_done");
   // slot 1: the quotients that need no other quotient
@@ -2263,6 +2314,10 @@ __device__ __forceinline__ void quad_rhs(const CachedStaticBG& B, const QuadRole
   }
   const double du = qbcast<0>(q1), dv = qbcast<0>(q2), dux = qbcast<1>(q1), dvx = qbcast<1>(q2);
   const double qu = qbcast<2>(q1), qv = qbcast<2>(q2), qk = qbcast<3>(q1), ql = qbcast<3>(q2);
+#if !RWRT_QUAD_MASK_BRANCH
+  const double fmu = mk ? du * m : du, fmv = mk ? dv * m : dv;
+  const double fmux = mk ? dux * m : dux, fmvx = mk ? dvx * m : dvx;
+#else
   double fmu = du, fmv = dv, fmux = dux, fmvx = dvx;
   if (RARE(mk)) {
     asm volatile("");   // the pole band (rare branch)
@@ -2271,6 +2326,7 @@ __device__ __forceinline__ void quad_rhs(const CachedStaticBG& B, const QuadRole
     fmux = dux * m;
     fmvx = dvx * m;
   }
+#endif
   const double ug = fmu + qu, vg = fmv + qv;                       // cal_ugvg (wn.py:266-294)
   const double dzwn = (-kx) * ((fmux + kap * fmvx) + qk);          // core_diffun (wr.py:53-78)
   const double dmwn = (-kx) * ((fmuy + kap * fmvy) + ql);
@@ -2575,8 +2631,11 @@ __device__ __forceinline__ void quad_rays(const RunArgs<StaticBG>& a, char* cach
 using KStore = KShared<5>;
 // kTrace: the diagnostic instantiation (rwrt_ctx_set_trace) -- the product
 // kernel carries none of the trace hooks
+#ifndef RWRT_RUN_ALIGN
+#define RWRT_RUN_ALIGN 256
+#endif
 template <class BG, bool kTrace = false>
-__global__ void __launch_bounds__(256, 1) rk45_run_kernel(RunArgs<BG> a) {
+__global__ void __launch_bounds__(256, 1) __attribute__((aligned(RWRT_RUN_ALIGN))) rk45_run_kernel(RunArgs<BG> a) {
   nm_stage<NM_ALL>();
   using LBG = typename LaneBG<BG>::type;
   using RayProblem = RayProblemT<LBG>;
@@ -2855,23 +2914,10 @@ frozen_tail_kernel(RunArgs<BG> a, double* __restrict__ tail_row) {
   }
 }
 
-// rwrt_expand_tails: rows [tail_from[j], it_end) of every ray j := tail_row[j],
-// one 16-B quarter of a row per thread (coalesced; rows without a tail untouched)
-__global__ void expand_tails_kernel(double* __restrict__ out, int64_t nray, int32_t it_begin, int32_t nrows,
-                                    const int32_t* __restrict__ tail_from, const double* __restrict__ tail_row) {
-  const int64_t per = (int64_t)nrows * 4, n = nray * per;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t j = i / per;
-    const int64_t q = i - j * per;
-    if (it_begin + (int32_t)(q >> 2) >= tail_from[j])
-      reinterpret_cast<double2*>(out)[i] = reinterpret_cast<const double2*>(tail_row)[j * 4 + (q & 3)];
-  }
-}
 
 
 __global__ void math_kernel(int kind, int64_t n, const double* __restrict__ x,
-                            const double* __restrict__ y, double* __restrict__ out,
-                            double cut_a = 0.0) {
+                            const double* __restrict__ y, double* __restrict__ out) {
   nm_stage<NM_ALL>();
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -2912,15 +2958,6 @@ __global__ void math_kernel(int kind, int64_t n, const double* __restrict__ x,
       G.num(a);
       G.den(b);
       r = G.ok() ? 1.0 : 0.0;
-    } break;
-    case 36:     // the jump mask's verdict (1: jump) for a step of (dlat, dlon) = (a, b) from
-    case 37: {   // (lon, lat) = (1.0, 0.6), cut_off 0.05 rad: 36 with the fast verdict, 37 without
-      const double lat_p = 0.6, lon_p = 1.0, cut = 0.05;
-      const double lat_c = lat_p + a, lon_c = lon_p + b;
-      const double cp = k_cos(lat_p), cc = k_cos(lat_c), ca = cut_a;   // haversine_cut(0.05), host
-      const bool j = (kind == 36) ? cal_dis_reaches<true>(lon_c, lat_c, lon_p, lat_p, cc, cp, cut, ca)
-                                  : cal_dis_reaches<false>(lon_c, lat_c, lon_p, lat_p, cc, cp, cut, ca);
-      r = j ? 1.0 : 0.0;
     } break;
     default: r = kNaN; break;   // (unreachable: rwrt_selftest_math rejects other kinds)
   }
@@ -3325,7 +3362,6 @@ struct rwrt_ctx {
   hipEvent_t flagged = nullptr, filled = nullptr;
   hipEvent_t done = nullptr;   // end of the last call on this context
   int quad_per_wave = 16;      // latency mode: rays per wave (rwrt_ctx_set_latency_density)
-  int reserved_cus = 0;        // CUs the persistent grid leaves free (rwrt_ctx_set_reserved_cus)
   int64_t* trace = nullptr;    // rwrt_ctx_set_trace (diagnostic)
   int64_t trace_cap = 0;
   bool used = false;
@@ -3456,7 +3492,6 @@ rwrt_status launch_run(rwrt_ctx* ctx, const BG& B, int64_t nray, const rwrt_para
   // latency-mode grid and launching it
   std::lock_guard<std::mutex> lock(ctx->mu);
   const int32_t quad_per_wave = ctx->quad_per_wave;
-  const int64_t reserved = ctx->reserved_cus;
   const int64_t per_block = 4 * (int64_t)quad_per_wave;   // rays per latency-mode block
   const int64_t team_blocks = (n_heavy + per_block - 1) / per_block;
   if (team_blocks > ctx->ncu / 2)
@@ -3469,8 +3504,7 @@ rwrt_status launch_run(rwrt_ctx* ctx, const BG& B, int64_t nray, const rwrt_para
   int64_t blocks = ctx_persistent_blocks<BG>(ctx);
   // latency-mode blocks take a CU each (their LDS does not fit beside a
   // persistent block): the persistent grid shrinks by as many CUs
-  // (and CUs reserved for a concurrent call on another context: rwrt_ctx_set_reserved_cus)
-  if (team_blocks + reserved) blocks = std::max<int64_t>(1, blocks - (team_blocks + reserved) * (blocks / ctx->ncu));
+  if (team_blocks) blocks = std::max<int64_t>(1, blocks - team_blocks * (blocks / ctx->ncu));
   const int64_t need = (nray - n_heavy + 255) / 256;
   if (blocks > need) blocks = need;
   RunArgs<BG> a{B, nray, p->rtol, p->atol, p->min_step, p->cut_off, p->nt, it_begin, it_end,
@@ -3663,6 +3697,37 @@ __global__ void rhs_bg_kernel(BG B, int64_t n, const double* __restrict__ t,
   }
 }
 
+// rwrt_expand_tails: rows [tail_from[j], it_end) of every ray j := tail_row[j],
+// one 16-B quarter of a row per thread (coalesced; rows without a tail untouched)
+__global__ void expand_tails_kernel(double* __restrict__ out, int64_t nray, int32_t it_begin, int32_t nrows,
+                                    const int32_t* __restrict__ tail_from, const double* __restrict__ tail_row) {
+  const int64_t per = (int64_t)nrows * 4, n = nray * per;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t j = i / per;
+    const int64_t q = i - j * per;
+    if (it_begin + (int32_t)(q >> 2) >= tail_from[j])
+      reinterpret_cast<double2*>(out)[i] = reinterpret_cast<const double2*>(tail_row)[j * 4 + (q & 3)];
+  }
+}
+
+// rwrt_selftest_math kinds 36/37: the jump mask's verdict (1: jump) for a step
+// of (dlat, dlon) = (x, y) from (lon, lat) = (1.0, 0.6), cut_off 0.05 rad:
+// 36 with the ray loops' polynomial "no jump" shortcut, 37 without it.
+// (Kernels added after round 4 are defined here, after the ray loops, so
+// that the ray loops keep their place in the code object.)
+__global__ void jump_verdict_kernel(int kind, int64_t n, const double* __restrict__ x,
+                                    const double* __restrict__ y, double* __restrict__ out, double cut_a) {
+  nm_stage<NM_SINCOS>();
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double lat_p = 0.6, lon_p = 1.0, cut = 0.05;
+  const double lat_c = lat_p + x[i], lon_c = lon_p + y[i];
+  const double cp = k_cos(lat_p), cc = k_cos(lat_c);
+  const bool j = (kind == 36) ? cal_dis_reaches<true>(lon_c, lat_c, lon_p, lat_p, cc, cp, cut, cut_a)
+                              : cal_dis_reaches<false>(lon_c, lat_c, lon_p, lat_p, cc, cp, cut, cut_a);
+  out[i] = j ? 1.0 : 0.0;
+}
+
 }  // namespace rwrt
 
 using namespace rwrt;
@@ -3702,14 +3767,6 @@ rwrt_status rwrt_ctx_set_latency_density(rwrt_ctx* c, int32_t rays_per_wave) {
   if (rays_per_wave < 1 || rays_per_wave > 16) return fail(RWRT_ERR_ARG, "rays_per_wave must be 1..16%s");
   std::lock_guard<std::mutex> lock(c->mu);
   c->quad_per_wave = rays_per_wave;
-  return RWRT_OK;
-}
-
-rwrt_status rwrt_ctx_set_reserved_cus(rwrt_ctx* c, int32_t cus) {
-  if (!c) return fail(RWRT_ERR_ARG, "rwrt_ctx is NULL%s");
-  if (cus < 0 || cus > c->ncu / 2) return fail(RWRT_ERR_ARG, "reserved CUs must be 0 .. half the device's CUs%s");
-  std::lock_guard<std::mutex> lock(c->mu);
-  c->reserved_cus = cus;
   return RWRT_OK;
 }
 
@@ -4015,9 +4072,14 @@ rwrt_status rwrt_selftest_math(int32_t kind, int64_t n, const double* d_x, const
   if (kind >= 17 && kind <= 22)   // retired device-libm restatements: never alias another kind
     return fail(RWRT_ERR_ARG, "selftest kinds 17-22 are retired%s");
   if (n == 0) return RWRT_OK;
-  if (kind >= 36 && !d_y) return fail(RWRT_ERR_ARG, "selftest kinds 36/37 need d_y%s");
+  if (kind >= 36) {
+    if (!d_y) return fail(RWRT_ERR_ARG, "selftest kinds 36/37 need d_y%s");
+    hipLaunchKernelGGL(jump_verdict_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, kind,
+                       n, d_x, d_y, d_out, haversine_cut(0.05));
+    return check_launch("jump_verdict_kernel");
+  }
   hipLaunchKernelGGL(math_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, kind,
-                     n, d_x, d_y, d_out, haversine_cut(0.05));
+                     n, d_x, d_y, d_out);
   return check_launch("math_kernel");
 }
 

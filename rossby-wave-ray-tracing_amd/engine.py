@@ -118,17 +118,6 @@ class RayEngine:
             self._ctx = H.Context(self.device)
         return self._ctx
 
-    _ctx_heavy = None
-
-    @property
-    def ctx_heavy(self):
-        """A second ``rwrt_ctx`` for a latency-mode call running beside this
-        engine's other calls on another stream (``shard.run_sharded``'s
-        ``heavy``): its own flags, side stream and events."""
-        if self._ctx_heavy is None:
-            self._ctx_heavy = H.Context(self.device)
-        return self._ctx_heavy
-
     def _stream(self):
         """The current stream of the engine's device (not torch's current device)."""
         return H.stream(self.device)
@@ -412,15 +401,11 @@ class RayEngine:
             return 0, 16
         return n_best, q_best
 
-    def run(self, st, p, tbound, it_begin, it_end, out, order=None, n_heavy=0, rays_per_wave=16, tails=None,
-            ctx=None, work=None):
+    def run(self, st, p, tbound, it_begin, it_end, out, order=None, n_heavy=0, rays_per_wave=16, tails=None):
         """Rows ``[it_begin, it_end)`` into ``out[nray, it_end-it_begin, 8]`` (async);
-        with ``tails`` (a ``Tails``) the frozen rays' constant rows go there instead.
-        ``ctx``: the context to run on (default: the engine's); ``work``: the
-        queue scratch (default: the engine's -- a call running concurrently
-        with another needs its own)."""
+        with ``tails`` (a ``Tails``) the frozen rays' constant rows go there instead."""
         lib = H.load()
-        ctx = ctx or self.ctx
+        ctx = self.ctx
         if n_heavy:
             ctx.set_latency_density(rays_per_wave)
         if self.bg is None:
@@ -432,7 +417,7 @@ class RayEngine:
                 H.dptr(st["state"]), H.dptr(st["count"]), H.dptr(st["nanrow"]), H.dptr(out, F64)]
         if tails is not None:
             args += [H.dptr(tails.frm, torch.int32), H.dptr(tails.row, F64)]
-        H.check(fn(*args, H.dptr(self.work if work is None else work), self._stream()))
+        H.check(fn(*args, H.dptr(self.work), self._stream()))
 
     def tails(self, nray):
         """A ``Tails`` for ``nray`` rays, or None when the engine writes dense rows."""

@@ -230,83 +230,6 @@ def cost_partition(cost, frozen, rank, world):
     return torch.sort(order[owner == rank]).values
 
 
-def _run_with_heavy(eng, local, idx, hv, p, tb, start, nt, keep, last, sink, chunk, out, events, group,
-                    order_policy, lead, n_live, team, split):
-    """run_sharded's rest of the horizon with the rays ``hv`` (local indices,
-    heaviest first) in one latency-mode call on ``eng.ctx_heavy`` and a second
-    stream, the other rays through ``eng.advance`` on the current stream; the
-    state, counters and last rows are merged back into ``local`` / ``last``."""
-    from engine import RunResult
-    dev = eng.device
-    n = local["nray"]
-    rest_mask = torch.ones(n, dtype=torch.bool, device=dev)
-    rest_mask[hv] = False
-    rest = torch.nonzero(rest_mask).squeeze(1)
-    st_h, st_r = eng.take(local, hv), eng.take(local, rest)
-    k = int(hv.numel())
-    cus = -(-k // 64)                                   # latency-mode blocks: 64 rays (16 per wave) per CU
-    out_h = torch.empty((k, nt - start, 8), dtype=torch.float64, device=dev)
-    work_h = torch.zeros(4, dtype=torch.int32, device=dev)
-    tails_h = eng.tails(k)
-    cur = torch.cuda.current_stream(dev)
-    side = torch.cuda.Stream(device=dev)
-    ready = torch.cuda.Event()
-    ready.record(cur)
-    with torch.cuda.stream(side):
-        side.wait_event(ready)
-        # (its own queue scratch: the two calls run at the same time)
-        eng.run(st_h, p, tb, start, nt, out_h, torch.arange(k, dtype=torch.int64, device=dev), k, 16,
-                tails=tails_h, ctx=eng.ctx_heavy, work=work_h)
-        done = torch.cuda.Event()
-        done.record(side)
-    rest_last = {}
-
-    def keep_rest(i0, i1, rows, tails=None):
-        rest_last["row"] = rows[:, -1] if tails is None else tails.last_row(rows, i1)
-        if sink is not None:
-            _deliver(eng, sink, i0, i1, rows, idx[rest], tails)
-    keep_rest.takes_tails = True
-    eng.ctx.set_reserved_cus(cus)
-    try:
-        res_r = eng.advance(st_r, p, tb, start, chunk=chunk, sink=keep_rest, out=out, events=events,
-                            group=None, order_policy=order_policy, first_chunk=list(lead), n_live=n_live,
-                            n_live_local=int((~torch.isnan(st_r["state"][:5].sum(0))).sum().item()),
-                            prev_work=torch.zeros_like(st_r["count"][:, 0]), team=team, split=split)
-    finally:
-        eng.ctx.set_reserved_cus(0)
-    cur.wait_event(done)
-    # merge the two halves back into the rank's state (checkpoints, counters, gather)
-    for key in ("count", "nanrow"):
-        local[key][rest] = st_r[key]
-        local[key][hv] = st_h[key]
-    local["state"][:, rest] = st_r["state"]
-    local["state"][:, hv] = st_h["state"]
-    row = torch.empty((n, 8), dtype=torch.float64, device=dev)
-    row[rest] = rest_last["row"]
-    row[hv] = out_h[:, -1] if tails_h is None else tails_h.last_row(out_h, nt)
-    last["row"] = row
-    if sink is not None:
-        _deliver(eng, sink, start, nt, out_h, idx[hv], tails_h)
-    mx = int(local["nanrow"].max().item()) if n else 0
-    mx = reduce_max(mx, group)
-    res = RunResult(local["count"][:, 0], local["count"][:, 1], local["nanrow"], False,
-                    mx if mx < int(p.nt) else None, n_live)
-    res.bounds = list(res_r.bounds)
-    res.state, res.next_row, res.params = local, res_r.next_row, res_r.params
-    res.heavy = {"rays": k, "cus": cus, "rows": [int(start), int(nt)]}
-    return res
-
-
-def _deliver(eng, sink, i0, i1, rows, ridx, tails):
-    """run_sharded's sink protocol: ``sink(i0, i1, rows, ridx[, tails])``."""
-    if tails is not None and getattr(sink, "takes_tails", False):
-        sink(i0, i1, rows, ridx, tails)
-    else:
-        if tails is not None:
-            eng.expand(rows, tails, i0, i1)
-        sink(i0, i1, rows, ridx)
-
-
 class ShardedRun:
     """Outcome of ``run_sharded`` on one rank."""
 
@@ -319,20 +242,9 @@ class ShardedRun:
         self.failed = failed
 
 
-def heavy_set(cost, frozen, k):
-    """The ``k`` live rays with the most probe attempts (local indices, heaviest
-    first; fewer if fewer are live): the rays whose chains of attempts bound
-    a split set's makespan."""
-    w = torch.where(frozen, torch.full_like(cost, -1), cost)
-    k = min(int(k), int((~frozen).sum().item()))
-    if k <= 0:
-        return None
-    return torch.sort(w, descending=True, stable=True).indices[:k]
-
-
 def run_sharded(eng, y0, nt, tstep=7200.0, group=None, rank=None, world=None, probe=6,
                 lead=(24, 96), chunk=None, out=None, sink=None, events=None, gather=True,
-                ttotal=None, order_policy="priority", team=0, split=None, heavy=0):
+                ttotal=None, order_policy="priority", team=0, split=None):
     """One ray set ``y0[5, nray]`` (identical on every rank) integrated across
     the ranks of ``group``.
 
@@ -343,12 +255,7 @@ def run_sharded(eng, y0, nt, tstep=7200.0, group=None, rank=None, world=None, pr
     their last row and step counters to rank 0 (RCCL ``gather`` on device
     tensors).  ``sink(i0, i1, rows, idx)`` receives this rank's rows.
     ``team`` is ``RayEngine.advance``'s latency-mode size per launch, ``split``
-    its adaptive split of the long launch.  ``heavy`` > 0 (static background):
-    this rank's ``heavy`` rays with the most probe attempts run the whole rest
-    of the horizon in ONE latency-mode call (quad_rays) on a second context
-    and stream, beside the launches of the other rays (whose persistent grids
-    leave it its CUs) -- no launch boundary ever stalls the chains that bound
-    the makespan.
+    its adaptive split of the long launch.
     ``rank``/``world`` without a group emulate one rank of a larger job on
     this device (single-GPU rehearsal: no collectives).  Rays are independent
     and both global couplings are decided over every ray, so the union of the
@@ -383,21 +290,22 @@ def run_sharded(eng, y0, nt, tstep=7200.0, group=None, rank=None, world=None, pr
     def keep(i0, i1, rows, tails=None):
         # the endpoints need each ray's last row only: a frozen ray's is its tail
         last["row"] = rows[:, -1] if tails is None else tails.last_row(rows, i1)
-        if sink is not None:
-            _deliver(eng, sink, i0, i1, rows, idx, tails)
+        if sink is None:
+            return
+        if tails is not None and getattr(sink, "takes_tails", False):
+            sink(i0, i1, rows, idx, tails)
+        else:
+            if tails is not None:
+                eng.expand(rows, tails, i0, i1)   # (a sink that wants the rows dense)
+            sink(i0, i1, rows, idx)
     keep.takes_tails = True
 
     keep(1, 1 + npr, prow[idx], None if ptails is None else ptails.take(idx))
     n_live_local = int((~frozen[idx]).sum().item())
-    hv = heavy_set(cost[idx], frozen[idx], heavy) if (heavy and eng.bg is None and 1 + npr < nt) else None
-    if hv is None:
-        res = eng.advance(local, p, tb, 1 + npr, chunk=chunk, sink=keep, out=out, events=events,
-                          group=group, order_policy=order_policy, first_chunk=list(lead),
-                          n_live=int(summary[0]), n_live_local=n_live_local,
-                          prev_work=torch.zeros_like(cost[idx]), team=team, split=split)
-    else:
-        res = _run_with_heavy(eng, local, idx, hv, p, tb, 1 + npr, nt, keep, last, sink, chunk, out, events,
-                              group, order_policy, lead, int(summary[0]), team, split)
+    res = eng.advance(local, p, tb, 1 + npr, chunk=chunk, sink=keep, out=out, events=events,
+                      group=group, order_policy=order_policy, first_chunk=list(lead),
+                      n_live=int(summary[0]), n_live_local=n_live_local,
+                      prev_work=torch.zeros_like(cost[idx]), team=team, split=split)
     steps_local = int(local["count"][:, 0].sum().item())
     ends = cnts = None
     if gather:

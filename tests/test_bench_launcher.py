@@ -100,7 +100,7 @@ def test_schedule_defaults():
     import bench
 
     def ns(**kw):
-        base = dict(config="C3", scaling="weak", bg="zonal", first_chunk=None, probe=None, team=None, heavy=None)
+        base = dict(config="C3", scaling="weak", bg="zonal", first_chunk=None, probe=None, team=None)
         base.update(kw)
         return argparse.Namespace(**base)
     a = bench.schedule_defaults(ns(), 1)
@@ -108,9 +108,9 @@ def test_schedule_defaults():
     a = bench.schedule_defaults(ns(bg="nonzonal"), 8)
     assert (a.first_chunk, a.probe, a.team) == ("24,160", 4, "0")
     a = bench.schedule_defaults(ns(scaling="strong"), 8)
-    assert (a.first_chunk, a.probe, a.team, a.heavy) == ("24,96", 6, "auto", 128)   # a split set
+    assert (a.first_chunk, a.probe, a.team) == ("24,96", 6, "auto")
     a = bench.schedule_defaults(ns(scaling="strong"), 1)
-    assert (a.first_chunk, a.probe, a.team, a.heavy) == ("24,160", 4, "64,64,64", 0)
+    assert (a.first_chunk, a.probe, a.team) == ("24,160", 4, "64,64,64")
     a = bench.schedule_defaults(ns(config="C5"), 1)
     assert (a.first_chunk, a.probe, a.team) == ("24,96", 6, "auto")
     a = bench.schedule_defaults(ns(probe=6, team="0", first_chunk="24"), 1)

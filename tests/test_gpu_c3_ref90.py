@@ -29,7 +29,7 @@ from make_devmath import row_hashes  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 
-def run_c3_90d(kind, team="auto", probe=6, split=None, info=None, heavy=0):
+def run_c3_90d(kind, team="auto", probe=6, split=None, info=None):
     """Rows [7, 1081, n] and (nacc, nrej) of the fixture's sample, from a
     full-set 90-day run with the bench's schedule.  ``info`` (a dict, if given)
     receives the engine's long-launch split decision."""
@@ -59,10 +59,9 @@ def run_c3_90d(kind, team="auto", probe=6, split=None, info=None, heavy=0):
         hist[:, i0:i1, p[m].cpu().numpy()] = np.transpose(got, (2, 1, 0))
 
     r = run_sharded(eng, rows0[:5].contiguous(), nt, 7200.0, rank=0, world=1, probe=probe, lead=[24, 160],
-                    chunk=nt - 1, sink=sink, ttotal=(nt - 1) * 7200.0, team=team, split=split, heavy=heavy)
+                    chunk=nt - 1, sink=sink, ttotal=(nt - 1) * 7200.0, team=team, split=split)
     if info is not None:
-        info.update(split_rho=eng.split_rho, threshold=eng.SPLIT_RHO, bounds=list(r.res.bounds),
-                    heavy=getattr(r.res, "heavy", None), heavy_idx=r.idx)
+        info.update(split_rho=eng.split_rho, threshold=eng.SPLIT_RHO, bounds=list(r.res.bounds))
     counts = torch.empty((rows0.shape[1], 2), dtype=torch.int64, device=eng.device)
     counts[r.idx] = r.counts
     counts = counts[idx].cpu().numpy()
@@ -135,15 +134,3 @@ def test_c3_90d_sample_rk4_bitwise(kind):
     torch.cuda.empty_cache()
     bad = np.nonzero(row_hashes(hist) != g["rk4_row_sha"])[0]
     assert not bad.size, f"{bad.size} of {nt} RK4 rows differ, first row {int(bad[0])}"
-
-
-def test_c3_90d_sample_heavy_stream_bitwise():
-    """The split-set schedule's concurrent heavy call (shard.run_sharded
-    heavy=256: the 256 rays with the most probe attempts integrated over the
-    whole rest of the horizon in ONE latency-mode call on a second context and
-    stream, beside the launches of the rest): every row and count of the
-    sample bitwise, the merged endpoints and the early-exit row included."""
-    info = {}
-    g, hist, counts = run_c3_90d("zonal", team="auto", heavy=256, info=info)
-    check(g, hist, counts)
-    assert info["heavy"] and info["heavy"]["rays"] == 256 and info["heavy"]["cus"] == 4, info["heavy"]

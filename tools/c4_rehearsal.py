@@ -78,8 +78,6 @@ def main():
     ap.add_argument("--config", default="C3", choices=["C3", "C5"])
     ap.add_argument("--fields", default="fp64", choices=["fp64", "fp32"], help="C5: level storage")
     ap.add_argument("--reps", type=int, default=2)
-    ap.add_argument("--heavy", type=int, default=0,
-                    help="rays per rank in one whole-horizon latency-mode call beside the rest (bench --heavy)")
     a = ap.parse_args()
     # 'auto', an int (rays per launch at 16 per wave) or n:q (n rays at q per wave)
     team = a.team if a.team == "auto" else (tuple(int(x) for x in a.team.split(":")) if ":" in a.team
@@ -95,19 +93,16 @@ def main():
         bs, bg = bench.make_bs(a.bg)
         y0 = torch.as_tensor(bench.c3_initial_state(bs), device="cuda")
         eng = RayEngine.from_bs(bs)
-    out = {"config": a.config, "heavy": a.heavy, "days": a.days, "bg": a.bg if a.config == "C3" else "C5 time-varying",
+    out = {"config": a.config, "days": a.days, "bg": a.bg if a.config == "C3" else "C5 time-varying",
            "fields": a.fields if a.config == "C5" else "fp64", "team": a.team, "lead": a.lead,
            "nslot": int(y0.shape[1]), "live": int((~torch.isnan(y0.sum(0))).sum().item()), "worlds": {}}
     for w in [int(x) for x in a.worlds.split(",")]:
         ranks = []
         for r in range(w):
-            hv = a.heavy if w > 1 or a.heavy < 0 else 0
-            hv = abs(hv)
             dt, res = timed(lambda: run_sharded(eng, y0, nt, rank=r, world=w, gather=False,
-                                                       team=team, lead=lead, heavy=hv, **kw), reps=a.reps)
+                                                       team=team, lead=lead, **kw), reps=a.reps)
             ev = []
-            run_sharded(eng, y0, nt, rank=r, world=w, gather=False, team=team, lead=lead, events=ev, heavy=hv,
-                        **kw)
+            run_sharded(eng, y0, nt, rank=r, world=w, gather=False, team=team, lead=lead, events=ev, **kw)
             torch.cuda.synchronize()
             launches = [dict(d, ms=a_.elapsed_time(b_)) for d, (a_, b_) in
                         zip([{"rows": [1, 1 + 6], "n_heavy": 0, "per_wave": 16}] + list(eng.launch_log), ev)]
