@@ -60,9 +60,17 @@ constexpr double kOmega = 7.2921e-5;   // constants.py omega
 __device__ __forceinline__ double div_rearth(double x) { return x / kREarth; }
 constexpr double kNaN = __builtin_nan("");
 
-// Output rows are written once and never read back by the kernels: stores
-// marked non-temporal stream past the L2 instead of evicting the basic state
-// and solver state the ray loop re-reads.
+// Output rows are written once and never read back by the kernels.  The ray
+// loops store a ray's 64-B row with plain (write-back) stores: the L2 merges
+// the four 16-B pieces -- and a ray's next row, the other half of the 128-B
+// line -- before writing back, so HBM sees the row bytes (1.16x).  Marked
+// non-temporal they streamed past the L2 as partial writes, 2.4x the row
+// bytes, and the step was 1 % slower (round 5, profiles/r5/rows/).
+// (RWRT_ROW_NT=1: non-temporal row stores, A/B build.)  frozen_fill_kernel's
+// coalesced full-line stores stay non-temporal.
+#ifndef RWRT_ROW_NT
+#define RWRT_ROW_NT 0
+#endif
 typedef double v2f64 __attribute__((ext_vector_type(2)));
 template <bool NT>
 __device__ __forceinline__ void store_row16(double2* o, double2 v) {
@@ -986,6 +994,22 @@ struct LaneBG<VaryingBGA32> {
     return c;
   }
 };
+// RWRT_TV64_TWO_WAVES: the fp64 time-varying ray loop at two waves per SIMD
+// without the lower level's LDS cache (two blocks' caches do not fit a CU's
+// LDS): a second wave to hide the level gathers' latency (A/B build)
+#ifndef RWRT_TV64_TWO_WAVES
+#define RWRT_TV64_TWO_WAVES 0
+#endif
+template <class BG>
+struct RunWaves {
+  static constexpr int kPerSimd = 1;
+};
+#if RWRT_TV64_TWO_WAVES
+template <>
+struct RunWaves<VaryingBG<double>> {
+  static constexpr int kPerSimd = 2;
+};
+#else
 template <>
 struct LaneBG<VaryingBG<double>> {
   using type = CachedVaryingBG64;
@@ -995,6 +1019,7 @@ struct LaneBG<VaryingBG<double>> {
     return CachedVaryingBG64{B, lds + wave * kCacheBytesPerWave, (threadIdx.x & 63u) * 16u, ~0u, ~0u, -1};
   }
 };
+#endif
 
 }  // namespace rwrt
 
@@ -2591,10 +2616,10 @@ __device__ __forceinline__ void quad_rays(const RunArgs<StaticBG>& a, char* cach
       // holds the cache image the refills read
       for (int kr = it; kr < last; ++kr) {
         double2* o = reinterpret_cast<double2*>(a.out + ((size_t)ray * nrows + (kr - a.it_begin)) * RWRT_NOUT);
-        store_row16<1>(o + 0, r0);
-        store_row16<1>(o + 1, r1);
-        store_row16<1>(o + 2, r2);
-        store_row16<1>(o + 3, r3);
+        store_row16<RWRT_ROW_NT>(o + 0, r0);
+        store_row16<RWRT_ROW_NT>(o + 1, r1);
+        store_row16<RWRT_ROW_NT>(o + 2, r2);
+        store_row16<RWRT_ROW_NT>(o + 3, r3);
       }
     }
     if (nanrow == a.nt && isnan(y[0])) nanrow = it;   // wr.py:853-855 (host reduces)
@@ -2635,7 +2660,8 @@ using KStore = KShared<5>;
 #define RWRT_RUN_ALIGN 256
 #endif
 template <class BG, bool kTrace = false>
-__global__ void __launch_bounds__(256, 1) __attribute__((aligned(RWRT_RUN_ALIGN))) rk45_run_kernel(RunArgs<BG> a) {
+__global__ void __launch_bounds__(256, RunWaves<BG>::kPerSimd) __attribute__((aligned(RWRT_RUN_ALIGN)))
+rk45_run_kernel(RunArgs<BG> a) {
   nm_stage<NM_ALL>();
   using LBG = typename LaneBG<BG>::type;
   using RayProblem = RayProblemT<LBG>;
@@ -2740,10 +2766,10 @@ __global__ void __launch_bounds__(256, 1) __attribute__((aligned(RWRT_RUN_ALIGN)
       // holds the basic state (+0.5 % on C3, profiles/r3/sched/pass_aa_nt_rows.txt;
       // no row stores at all would be +3.3 %)
       double2* o = reinterpret_cast<double2*>(a.out + ((size_t)ray * nrows + (it - a.it_begin)) * RWRT_NOUT);
-      store_row16<1>(o + 0, r0);
-      store_row16<1>(o + 1, r1);
-      store_row16<1>(o + 2, r2);
-      store_row16<1>(o + 3, r3);
+      store_row16<RWRT_ROW_NT>(o + 0, r0);
+      store_row16<RWRT_ROW_NT>(o + 1, r1);
+      store_row16<RWRT_ROW_NT>(o + 2, r2);
+      store_row16<RWRT_ROW_NT>(o + 3, r3);
     }
     if (RARE(last > it + 1)) {
       asm volatile("");   // frozen: the remaining rows of the chunk (rare branch)
