@@ -1068,6 +1068,7 @@ __device__ __forceinline__ double add_rd(double a, double b) {
 #define NM_ADD_RD(a, b) ::rwrt::add_rd((a), (b))
 #define NM_ISSUE_FENCE() __builtin_amdgcn_sched_barrier(0)
 #define NM_RARE(c) RARE(c)
+#define NM_RARE_ANY(c) RARE(__builtin_amdgcn_ballot_w64(c) != 0)
 #define NM_FALLBACK_SIN(x) ::sin(x)
 #define NM_FALLBACK_COS(x) ::cos(x)
 #define NM_FALLBACK_TAN(x) ::tan(x)
@@ -2565,8 +2566,10 @@ __device__ __forceinline__ void quad_rays(const RunArgs<StaticBG>& a, char* cach
       const double ha = fabs(h);
       double yn[5], k6[5];
       double en = quad_attempt(B, R, K, y, f, h, a.rtol, a.atol, yn, k6, aux);
+      MARK("attempt_done");
       if (en != en) en = 0.0;
       const double sp = kSafety * k_pow(en, kErrExp);
+      MARK("pow_done");
       const bool acc = en < 1.0;
       double fac = np_min(kMaxFactor, sp);
       if (en == 0.0) fac = kMaxFactor;
@@ -2584,10 +2587,12 @@ __device__ __forceinline__ void quad_rays(const RunArgs<StaticBG>& a, char* cach
       rejected = rejected || !acc;
       nacc += acc ? 1 : 0;
       nrej += acc ? 0 : 1;
+      MARK("control_done");
       if (!(acc && t - tb >= 0.0)) continue;
       st = 1;
     }
     // ---- interval it reached: rk45_run_kernel's post-processing (wr.py:835-885)
+    MARK("row_end");
     const bool have = !isnan(aux[2]);
     double ug, vg, cos_c = kNaN;
     bool masked = fabs(y[1]) >= kHalfPi;
@@ -2612,8 +2617,6 @@ __device__ __forceinline__ void quad_rays(const RunArgs<StaticBG>& a, char* cach
     if (writer) {
       const double2 r0 = make_double2(y[0], y[1]), r1 = make_double2(y[2], y[3]);
       const double2 r2 = make_double2(y[4], ug), r3 = make_double2(vg, (double)nacc);
-      // non-temporal, like the run kernel's: rows stream past the L2 that
-      // holds the cache image the refills read
       for (int kr = it; kr < last; ++kr) {
         double2* o = reinterpret_cast<double2*>(a.out + ((size_t)ray * nrows + (kr - a.it_begin)) * RWRT_NOUT);
         store_row16<RWRT_ROW_NT>(o + 0, r0);

@@ -78,6 +78,7 @@ def main():
     ap.add_argument("--config", default="C3", choices=["C3", "C5"])
     ap.add_argument("--fields", default="fp64", choices=["fp64", "fp32"], help="C5: level storage")
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--chunk", type=int, default=0, help="C5: rows per launch (default: bench.py's, 48 fp64 / 240 fp32)")
     a = ap.parse_args()
     # 'auto', an int (rays per launch at 16 per wave) or n:q (n rays at q per wave)
     team = a.team if a.team == "auto" else (tuple(int(x) for x in a.team.split(":")) if ":" in a.team
@@ -87,13 +88,14 @@ def main():
     kw = {}
     if a.config == "C5":
         eng, y0, chunk = c5_setup(a, nt)
+        chunk = a.chunk or chunk
         kw = dict(chunk=chunk, order_policy="cell", ttotal=(nt - 1) * 7200.0)
         team = 0
     else:
         bs, bg = bench.make_bs(a.bg)
         y0 = torch.as_tensor(bench.c3_initial_state(bs), device="cuda")
         eng = RayEngine.from_bs(bs)
-    out = {"config": a.config, "days": a.days, "bg": a.bg if a.config == "C3" else "C5 time-varying",
+    out = {"config": a.config, "chunk": a.chunk or None, "days": a.days, "bg": a.bg if a.config == "C3" else "C5 time-varying",
            "fields": a.fields if a.config == "C5" else "fp64", "team": a.team, "lead": a.lead,
            "nslot": int(y0.shape[1]), "live": int((~torch.isnan(y0.sum(0))).sum().item()), "worlds": {}}
     for w in [int(x) for x in a.worlds.split(",")]:
