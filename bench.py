@@ -722,6 +722,20 @@ def c5_parity_sample(eng, rows_all, fields, dev):
     return out
 
 
+def c5_rows_per_launch(fp32, world, nt):
+    """C5's rows per launch of the long launches (before the memory cap):
+    fp32 levels 240 (profiles/r1/c5/chunk_sweep.txt); fp64 levels, 32 rays per
+    wave with both levels cached (RayEngine.tv_lanes), 144 on one GPU (72 /
+    96 / 144 / 192 rows: 2.72 / 2.70 / 2.69 / 2.81 s) and the whole rest of
+    the horizon when a set is split (N = 2 / 4 / 8: 1.67-1.72 / 0.99 / 0.78 s
+    against 1.90 / 1.52 / 1.34 s at 96-row or 48-row launches: a shard's
+    heaviest rays then run their chains without a barrier;
+    profiles/r5/sched/c5_half_*.json)."""
+    if fp32:
+        return 240
+    return 144 if world <= 1 else nt - 1
+
+
 def main_c5(args, dist, group, rank, world, dev, share=1):
     """BASELINE configs[4]: a 0.25-degree time-varying background (one level
     every 6 h, built on the device by rwrt_bs_ready, fp64 or fp32 storage) and
@@ -773,13 +787,11 @@ def main_c5(args, dist, group, rank, world, dev, share=1):
     y0 = make_y0()
     nslot = y0.shape[1]
     n_live = int((~torch.isnan(y0.sum(0))).sum().item())
-    # rows per launch (measured, profiles/r1/c5/chunk_sweep.txt and
-    # profiles/r1/v7/c5/): fp64 levels want a short time window (4 days: 17
-    # levels in flight), fp32 levels 20-day windows
+    # rows per launch: c5_rows_per_launch, capped by the row buffer's memory
     n_local = nslot if weak else -(-nslot // world) + 2
     free = torch.cuda.mem_get_info(dev)[0] // share
     cap = max(1, min(nt - 1, int(0.8 * free) // (n_local * 64)))
-    chunk = min(args.chunk or (240 if lv.fp32 else 48), cap)
+    chunk = min(args.chunk or c5_rows_per_launch(lv.fp32, 1 if weak else world, nt), cap)
     out = torch.empty((n_local, min(chunk, nt - 1), 8), dtype=torch.float64, device=dev)
     lead = [int(x) for x in str(args.first_chunk).split(",") if x]
 

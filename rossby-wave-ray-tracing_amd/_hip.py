@@ -14,7 +14,7 @@ LIB_PATH = os.environ.get("RWRT_LIB", os.path.join(_HERE, "librwrt.so"))
 
 NFIELD_REF, NFIELD_PACK, NVAR, NMERC, NOUT, NSTATE = 18, 12, 5, 12, 8, 12
 ABI_SYMBOLS = ("rwrt_version", "rwrt_last_error", "rwrt_ctx_create", "rwrt_ctx_destroy",
-               "rwrt_ctx_set_latency_density", "rwrt_ctx_set_trace",
+               "rwrt_ctx_set_latency_density", "rwrt_ctx_set_tv_lanes", "rwrt_ctx_set_trace",
                "rwrt_pack_fields",
                "rwrt_mercator_point", "rwrt_rhs", "rwrt_dp54_attempt",
                "rwrt_ray_initial", "rwrt_rk45_init", "rwrt_rk45_run", "rwrt_rk45_run_tails",
@@ -91,6 +91,7 @@ def load():
         "rwrt_ctx_create": [_I32, ctypes.POINTER(_P)],
         "rwrt_ctx_destroy": [_P],
         "rwrt_ctx_set_latency_density": [_P, _I32],
+        "rwrt_ctx_set_tv_lanes": [_P, _I32],
         "rwrt_ctx_set_trace": [_P, _P, _I64],
         "rwrt_rhs_tv": [G, B, _I64, _P, _P, _P, _P],
         "rwrt_kat_rk45": [_I32, _I64, _P, _I32, _P, _D, _D, _D, _P, _P],
@@ -162,6 +163,12 @@ class Context:
         if getattr(self, "_qpw", 16) != int(rays_per_wave):
             check(load().rwrt_ctx_set_latency_density(self._h, int(rays_per_wave)))
             self._qpw = int(rays_per_wave)
+
+    def set_tv_lanes(self, lanes):
+        """Rays per wave of the fp64 time-varying loops, 64 or 32 (rwrt_ctx_set_tv_lanes)."""
+        if getattr(self, "_tvl", 64) != int(lanes):
+            check(load().rwrt_ctx_set_tv_lanes(self._h, int(lanes)))
+            self._tvl = int(lanes)
 
     def set_trace(self, trace=None):
         """Diagnostic ray trace (rwrt_ctx_set_trace): ``trace`` an int64 device

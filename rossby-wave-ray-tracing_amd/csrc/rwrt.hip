@@ -660,6 +660,7 @@ struct VaryingBG {
   static constexpr bool kTimeVarying = true;
   const T* __restrict__ P;   // [nlev][W][H][12]
   int W, H, nlev;
+  int half;                  // fp64 ray loop at 32 rays per wave, both levels cached (rwrt_ctx_set_tv_lanes)
   int64_t lev_stride;        // W * H * 12
   double lon0, dlon, lat0, dlat, t0, dt;
 
@@ -902,6 +903,7 @@ struct CachedVaryingBG64 {
     int jl;
     V.cell(lon, lat, p.o, p.w, kx, ky);
     const double* A = V.level(t, p.wt, jl);
+    p.B = A + (V.nlev > 1 ? V.lev_stride : 0);
     if (kx != key_x || ky != key_y || jl != key_j) {   // miss: refill by LDS-DMA
       char* const base = lds_slice_base(wave_base);
 #pragma unroll
@@ -910,16 +912,47 @@ struct CachedVaryingBG64 {
         for (int q = 0; q < 6; ++q)
           __builtin_amdgcn_global_load_lds((global_void_ptr)(A + p.o[j] + 2 * q),
                                            (lds_void_ptr)(base + (j * 6 + q) * 1024), 16, 0, 0);
+      if (V.half) {   // (wave-uniform) the upper level into lanes 32-63's slots
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int q = 0; q < 6; ++q)
+            __builtin_amdgcn_global_load_lds((global_void_ptr)(p.B + p.o[j] + 2 * q),
+                                             (lds_void_ptr)(base + (j * 6 + q) * 1024 + 512), 16, 0, 0);
+      }
       key_x = kx;
       key_y = ky;
       key_j = jl;
     }
-    p.B = A + (V.nlev > 1 ? V.lev_stride : 0);
     return p;
+  }
+  // the eleven blends of one level from the slice (lv 1: the upper level,
+  // half density only)
+  __device__ __forceinline__ void cached11(int lv, const double w[4], double g[11]) const {
+    double2 v[4][6];
+#pragma unroll
+    for (int q = 0; q < 6; ++q)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        v[j][q] = *reinterpret_cast<const double2*>(wave_base + (j * 6 + q) * 1024 + lv * 512 + lane16);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      g[2 * q] = VaryingBG<double>::bl(w, v[0][q].x, v[1][q].x, v[2][q].x, v[3][q].x);
+      if (2 * q + 1 < 11) g[2 * q + 1] = VaryingBG<double>::bl(w, v[0][q].y, v[1][q].y, v[2][q].y, v[3][q].y);
+    }
   }
   __device__ __forceinline__ void end(const Pending& p, double g[11]) const {
     lds_dma_wait();
     double gb[11];
+    if (V.half) {
+      double ga[11];
+      cached11(0, p.w, ga);
+      cached11(1, p.w, gb);
+#pragma unroll
+      for (int i = 0; i < 11; ++i) g[i] = ga[i] * (1.0 - p.wt) + gb[i] * p.wt;
+      return;
+    }
     V.blend_level<11>(p.B, p.o, p.w, 0, gb);
     double2 v[4][6];
 #pragma unroll
@@ -2683,6 +2716,9 @@ rk45_run_kernel(RunArgs<BG> a) {
       return;
     }
   }
+  if constexpr (std::is_same<BG, VaryingBG<double>>::value) {
+    if (a.B.half && (threadIdx.x & 63u) >= 32u) return;   // half density: lanes 32-63's LDS slots hold the upper level
+  }
   const RayProblem P{LaneBG<BG>::make(a.B, smem + kKBytes)};
   const int64_t nrows = a.it_end - a.it_begin;
   Lane<RayProblem, KStore> L;
@@ -3391,6 +3427,7 @@ struct rwrt_ctx {
   hipEvent_t flagged = nullptr, filled = nullptr;
   hipEvent_t done = nullptr;   // end of the last call on this context
   int quad_per_wave = 16;      // latency mode: rays per wave (rwrt_ctx_set_latency_density)
+  int tv_lanes = 64;           // rays per wave of fp64 time-varying calls (rwrt_ctx_set_tv_lanes)
   int64_t* trace = nullptr;    // rwrt_ctx_set_trace (diagnostic)
   int64_t trace_cap = 0;
   bool used = false;
@@ -3534,7 +3571,9 @@ rwrt_status launch_run(rwrt_ctx* ctx, const BG& B, int64_t nray, const rwrt_para
   // latency-mode blocks take a CU each (their LDS does not fit beside a
   // persistent block): the persistent grid shrinks by as many CUs
   if (team_blocks) blocks = std::max<int64_t>(1, blocks - team_blocks * (blocks / ctx->ncu));
-  const int64_t need = (nray - n_heavy + 255) / 256;
+  int64_t block_rays = 256;   // rays a block runs at once
+  if constexpr (BG::kTimeVarying) block_rays = B.half ? 128 : 256;
+  const int64_t need = (nray - n_heavy + block_rays - 1) / block_rays;
   if (blocks > need) blocks = need;
   RunArgs<BG> a{B, nray, p->rtol, p->atol, p->min_step, p->cut_off, p->nt, it_begin, it_end,
                 d_tbound, d_order, d_state, d_count, d_nanrow, d_out, d_work,
@@ -3603,6 +3642,7 @@ rwrt_status make_varying(const rwrt_grid* g, const rwrt_background* b, VaryingBG
   B.dlat = F.dlat;
   B.t0 = b->t0;
   B.dt = b->dt;
+  B.half = 0;
   return RWRT_OK;
 }
 
@@ -3799,6 +3839,14 @@ rwrt_status rwrt_ctx_set_latency_density(rwrt_ctx* c, int32_t rays_per_wave) {
   return RWRT_OK;
 }
 
+rwrt_status rwrt_ctx_set_tv_lanes(rwrt_ctx* c, int32_t lanes) {
+  if (!c) return fail(RWRT_ERR_ARG, "rwrt_ctx is NULL%s");
+  if (lanes != 32 && lanes != 64) return fail(RWRT_ERR_ARG, "time-varying lanes per wave must be 32 or 64%s");
+  std::lock_guard<std::mutex> lock(c->mu);
+  c->tv_lanes = lanes;
+  return RWRT_OK;
+}
+
 rwrt_status rwrt_ctx_set_trace(rwrt_ctx* c, int64_t* d_trace, int64_t capacity) {
   if (!c) return fail(RWRT_ERR_ARG, "rwrt_ctx is NULL%s");
   if (capacity < 0 || (capacity > 0 && !d_trace) || capacity > 0x7fffffffLL)
@@ -3983,8 +4031,14 @@ rwrt_status rwrt_rk45_run_tv_tails(rwrt_ctx* ctx, const rwrt_grid* g, const rwrt
     return launch_run(ctx, B, nray, p, d_tbound, it_begin, it_end, d_order, n_heavy, d_state, d_count,
                       d_nanrow, d_out, d_tail_from, d_tail_row, d_work, stream);
   }
+  int lanes = 64;
+  if (ctx) {
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    lanes = ctx->tv_lanes;
+  }
   VaryingBG<double> B;
   if (rwrt_status s = make_varying(g, b, B)) return s;
+  B.half = lanes == 32;
   return launch_run(ctx, B, nray, p, d_tbound, it_begin, it_end, d_order, n_heavy, d_state, d_count,
                     d_nanrow, d_out, d_tail_from, d_tail_row, d_work, stream);
 }

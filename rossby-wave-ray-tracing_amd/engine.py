@@ -88,6 +88,12 @@ class RayEngine:
     # once per launch and expanded only for sinks that want dense rows; False:
     # every row written by the launch itself (rwrt_rk45_run; A/B and tests)
     use_tails = os.environ.get("RWRT_TAILS", "1") != "0"
+    # rays per wave of the fp64 time-varying loops (rwrt_ctx_set_tv_lanes: 32
+    # caches both bracketing levels per ray, no HBM gathers while a ray stays
+    # in its cell and level pair; 64 caches the lower level only).  Schedule
+    # only.  32: C5 1.17 -> 1.24e9 on one GPU, 8 shards 1.42 -> 0.78 s
+    # (with the split set's long launches, bench.c5_rows_per_launch)
+    tv_lanes = int(os.environ.get("RWRT_TV_LANES", "32"))
 
     def __init__(self, fields, lon, lat, device=None):
         """``fields``: the reference stack ``[nlon(+1), nlat, 18]`` (numpy or tensor);
@@ -406,6 +412,8 @@ class RayEngine:
         with ``tails`` (a ``Tails``) the frozen rays' constant rows go there instead."""
         lib = H.load()
         ctx = self.ctx
+        if self.bg is not None:
+            ctx.set_tv_lanes(self.tv_lanes)
         if n_heavy:
             ctx.set_latency_density(rays_per_wave)
         if self.bg is None:

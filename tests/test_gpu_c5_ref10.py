@@ -25,8 +25,10 @@ from make_devmath import row_hashes  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("storage", ["fp64", "fp32"])
-def test_c5_10d_41_levels_bitwise_with_oracle(storage):
+@pytest.mark.parametrize("storage,lanes", [("fp64", 32), ("fp64", 64), ("fp32", 64)])
+def test_c5_10d_41_levels_bitwise_with_oracle(storage, lanes):
+    """``lanes``: rays per wave of the fp64 loop (rwrt_ctx_set_tv_lanes; 32
+    caches both bracketing levels per ray) -- a schedule, so the same bits."""
     import torch
     import synthetic as S
     from engine import RayEngine
@@ -40,6 +42,7 @@ def test_c5_10d_41_levels_bitwise_with_oracle(storage):
         bj = b0 if j == 0 else S.background_level(j, res=0.25)
         lv.set_level(j, bj["u"], bj["v"])
     eng = RayEngine.from_levels(lv)
+    eng.tv_lanes = lanes
     cfg = S.config("C5")
     deg2rad = np.pi / 180.0
     ix, iy = np.meshgrid(np.arange(cfg.nnx), np.arange(cfg.nny))
@@ -60,7 +63,8 @@ def test_c5_10d_41_levels_bitwise_with_oracle(storage):
         m = p >= 0
         hist[:, i0:i1, p[m].cpu().numpy()] = np.transpose(rows[m][:, :, :7].cpu().numpy(), (2, 1, 0))
 
-    chunk = 240 if lv.fp32 else 48          # bench.py main_c5's rows per launch
+    from bench import c5_rows_per_launch
+    chunk = c5_rows_per_launch(lv.fp32, 1, nt)   # bench.py main_c5's rows per launch
     r = run_sharded(eng, rows0[:5].contiguous(), nt, 7200.0, rank=0, world=1, probe=6, lead=[24, 96],
                     chunk=chunk, sink=sink, ttotal=(nt - 1) * 7200.0,
                     order_policy="cell")   # bench.py's C5 default queue order
@@ -95,6 +99,7 @@ def _c5_worker(rank, world, port, storage, q):
         from engine import RayEngine
         from levels import Levels
         from shard import broadcast_levels, gather_rows, run_sharded
+        from bench import c5_rows_per_launch
         g = np.load(os.path.join(here, "golden", f"c5_ref10_{storage}.npz"))
         nt, nlev = int(g["nt"]), int(g["nlev"])
         b0 = S.background_level(0, res=0.25)
@@ -118,7 +123,8 @@ def _c5_worker(rank, world, port, storage, q):
         r0 = rows0[:, torch.as_tensor(g["idx"], device=eng.device)]
         parts = []
         r = run_sharded(eng, r0[:5].contiguous(), nt, 7200.0, group=dist.group.WORLD, probe=6, lead=[24, 96],
-                        chunk=48 if storage == "fp64" else 240, ttotal=(nt - 1) * 7200.0, order_policy="cell",
+                        chunk=c5_rows_per_launch(storage == "fp32", world, nt), ttotal=(nt - 1) * 7200.0,
+                        order_policy="cell",
                         sink=lambda a, b, o, idx: parts.append(o[:, :, :7].cpu()))
         mine = torch.cat(parts, dim=1)                                   # (n_local, nt-1, 7)
         full = gather_rows(mine, r.idx.cpu().numpy(), r0.shape[1], group=dist.group.WORLD)

@@ -64,7 +64,7 @@ def c5_setup(a, nt):
     src = eng.sources(lon, lat)
     y0 = torch.cat([eng.initial_rows_dev(src, eng.zwn_tensor(cfg.zwn, S.c3_freq(P)))[0][:5].reshape(5, -1)
                     for P in S.C3_PERIODS_DAYS], dim=1)
-    return eng, y0.contiguous(), (240 if lv.fp32 else 48)
+    return eng, y0.contiguous(), bench.c5_rows_per_launch(lv.fp32, 1, nt)
 
 
 def main():
@@ -87,24 +87,29 @@ def main():
     nt = int(a.days * 12) + 1
     kw = {}
     if a.config == "C5":
-        eng, y0, chunk = c5_setup(a, nt)
-        chunk = a.chunk or chunk
-        kw = dict(chunk=chunk, order_policy="cell", ttotal=(nt - 1) * 7200.0)
+        eng, y0, _ = c5_setup(a, nt)
+        kw = dict(order_policy="cell", ttotal=(nt - 1) * 7200.0)
         team = 0
     else:
         bs, bg = bench.make_bs(a.bg)
         y0 = torch.as_tensor(bench.c3_initial_state(bs), device="cuda")
         eng = RayEngine.from_bs(bs)
-    out = {"config": a.config, "chunk": a.chunk or None, "days": a.days, "bg": a.bg if a.config == "C3" else "C5 time-varying",
+    out = {"config": a.config, "chunk": a.chunk or None, "tv_lanes": getattr(eng, "tv_lanes", None), "days": a.days, "bg": a.bg if a.config == "C3" else "C5 time-varying",
            "fields": a.fields if a.config == "C5" else "fp64", "team": a.team, "lead": a.lead,
            "nslot": int(y0.shape[1]), "live": int((~torch.isnan(y0.sum(0))).sum().item()), "worlds": {}}
     for w in [int(x) for x in a.worlds.split(",")]:
         ranks = []
+        kw_w = dict(kw)
+        if a.config == "C5":   # bench.py main_c5's rows per launch, capped by the row buffer's memory
+            torch.cuda.empty_cache()
+            n_local = -(-int(y0.shape[1]) // w) + 2
+            cap = max(1, int(0.8 * torch.cuda.mem_get_info()[0]) // (n_local * 64))
+            kw_w["chunk"] = min(a.chunk or bench.c5_rows_per_launch(a.fields == "fp32", w, nt), cap)
         for r in range(w):
             dt, res = timed(lambda: run_sharded(eng, y0, nt, rank=r, world=w, gather=False,
-                                                       team=team, lead=lead, **kw), reps=a.reps)
+                                                       team=team, lead=lead, **kw_w), reps=a.reps)
             ev = []
-            run_sharded(eng, y0, nt, rank=r, world=w, gather=False, team=team, lead=lead, events=ev, **kw)
+            run_sharded(eng, y0, nt, rank=r, world=w, gather=False, team=team, lead=lead, events=ev, **kw_w)
             torch.cuda.synchronize()
             launches = [dict(d, ms=a_.elapsed_time(b_)) for d, (a_, b_) in
                         zip([{"rows": [1, 1 + 6], "n_heavy": 0, "per_wave": 16}] + list(eng.launch_log), ev)]
@@ -115,7 +120,8 @@ def main():
                           "launches": launches})
         steps = sum(x["ray_steps"] for x in ranks)
         mk = max(x["s"] for x in ranks)
-        out["worlds"][str(w)] = {"makespan_s": mk, "rate": steps / mk, "ray_steps": steps, "ranks": ranks}
+        out["worlds"][str(w)] = {"makespan_s": mk, "rate": steps / mk, "ray_steps": steps,
+                                 "rows_per_launch": kw_w.get("chunk"), "ranks": ranks}
         print(json.dumps({"world": w, "makespan_s": mk, "rate": steps / mk}), flush=True)
     one1 = out["worlds"].get("1")
     if one1:
