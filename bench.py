@@ -272,7 +272,9 @@ def schedule_defaults(args, world):
     if args.probe is None:
         args.probe = 4 if whole else 6
     if args.team is None:
-        args.team = ("64,64,64" if args.bg == "zonal" else "0") if whole else "auto"
+        # (C5: none -- the rays that end a split C5 launch are not the heaviest
+        # of the launches before it, profiles/r5/c5lat/)
+        args.team = ("64,64,64" if args.bg == "zonal" else "0") if whole else ("0" if args.config == "C5" else "auto")
     return args
 
 
@@ -391,6 +393,9 @@ def main():
                          "an integer, one per launch after the probe (e.g. 64,256,64; the last "
                          "repeats) or 'auto' (RayEngine.team_size).  Default: 64,64,64 for a whole C3 "
                          "set per GPU, auto for a split one")
+    ap.add_argument("--shard-probe", type=int, default=1, choices=[0, 1],
+                    help="N > 1 (strong): each rank probes 1/N of the rays and the probe costs are "
+                         "all-gathered (shard.probe_costs; 0: every rank probes every ray)")
     ap.add_argument("--lib", default=None, help="alternative librwrt build (A/B timing)")
     ap.add_argument("--traffic", default=None, help="traffic.json (tools/pmc_traffic.py)")
     ap.add_argument("--valu-profile", default=None, help="valu.json (tools/pmc_valu.py)")
@@ -529,7 +534,7 @@ def main():
             return r
         return run_sharded(eng, y, nt, 7200.0, group=group, probe=args.probe, lead=lead,
                            chunk=chunk, out=out, events=events, ttotal=(nt - 1) * 7200.0,
-                           order_policy=args.order, team=team, split=split)
+                           order_policy=args.order, team=team, split=split, shard_probe=bool(args.shard_probe))
 
     for _ in range(args.warmup):
         one_step()
@@ -794,6 +799,11 @@ def main_c5(args, dist, group, rank, world, dev, share=1):
     chunk = min(args.chunk or c5_rows_per_launch(lv.fp32, 1 if weak else world, nt), cap)
     out = torch.empty((n_local, min(chunk, nt - 1), 8), dtype=torch.float64, device=dev)
     lead = [int(x) for x in str(args.first_chunk).split(",") if x]
+    # latency mode (the time-varying latency waves: one ray per wave on its 64
+    # lanes, BlockVaryingBG) for a split set's heaviest rays; one GPU's set is
+    # throughput-bound
+    team = 0 if (weak or world == 1) else (args.team if args.team == "auto" else
+                                          (int(args.team.split(":")[0]), 1) if ":" in args.team else int(args.team))
 
     def one_step(events=None):
         if weak:
@@ -802,7 +812,7 @@ def main_c5(args, dist, group, rank, world, dev, share=1):
                                order_policy=args.order)
         return run_sharded(eng, make_y0(), nt, 7200.0, group=group, probe=args.probe, lead=lead,
                            chunk=chunk, out=out, events=events, ttotal=(nt - 1) * 7200.0,
-                           order_policy=args.order)
+                           order_policy=args.order, team=team, shard_probe=bool(args.shard_probe))
 
     for _ in range(args.warmup):
         one_step()
@@ -856,6 +866,11 @@ def main_c5(args, dist, group, rank, world, dev, share=1):
                        "parallelism": (f"{world} rank(s), each its own C5 seed grid (shifted by rank/N deg)"
                                        if weak else f"one ray set over {world} GPU(s) (run_sharded, as C3/C4)")},
             "parity_sample_vs_oracle": parity,
+            # the whole set's last rows (one set at every N when strong: the same hash at N = 1, 2, ..)
+            "endpoints_rank0_sha256": endpoint_sha(r.endpoints) if (r.endpoints is not None and not weak) else None,
+            "latency_mode": (f"{team if team == 'auto' else team} (time-varying latency waves: one ray per wave "
+                             f"on its 64 lanes, BlockVaryingBG)" if team else "none"),
+            "launches": [dict(d) for d in eng.launch_log],
             "ray_steps_per_step": tot_steps / args.steps,
             "rejected_per_accepted": tot_rej * args.steps / max(tot_steps, 1),
             "levels_build_s": t_build,

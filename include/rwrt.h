@@ -190,9 +190,9 @@ rwrt_status rwrt_rk45_init(const rwrt_grid* g, const double* d_packed,
  * (rkf45.py:222-253,375-514), then masked (wr.py:838-850) and its group
  * velocity recomputed (wr.py:856-865).  Rays are taken from device work
  * queues in the order d_order[nray] (NULL = 0..nray-1); the first n_heavy
- * entries (live rays, static background only, at most 64 per CU on half the
- * CUs) run in latency mode -- four lanes of a wave per ray, in the first
- * blocks of the same grid (pass the rays expected to be slowest; 0 = none).
+ * entries (live rays, at most 4 x rays-per-wave per CU on half the CUs) run
+ * in latency mode -- four lanes of a wave per ray, in the first blocks of the
+ * same grid (pass the rays expected to be slowest; 0 = none).
  * Output row r of
  * ray j is d_out[(j*(it_end-it_begin) + r)*8 + {lon,lat,k,l,amp,ug,vg,nacc}].
  * d_state / d_count / d_nanrow carry the per-ray solver state across calls
@@ -290,6 +290,12 @@ rwrt_status rwrt_rk45_run_tv(rwrt_ctx* ctx, const rwrt_grid* g, const rwrt_backg
                              int64_t n_heavy, double* d_state, int64_t* d_count,
                              int32_t* d_nanrow, double* d_out, int32_t* d_work,
                              void* stream);
+/* n_heavy > 0 on a time-varying background (fp64 or fp32 levels; not with
+ * fp32 arithmetic, fp32 == 2): the first n_heavy rays of d_order (at most 4
+ * per CU on half the CUs) run one per wavefront, replicated on its 64 lanes,
+ * their lookups served from an 8 x 8-point block of both bracketing levels in
+ * the wave's LDS (reloaded by all 64 lanes at once) -- a schedule, results
+ * are unchanged (ABI 3). */
 /* rwrt_rk45_run_tv with constant row tails (as rwrt_rk45_run_tails). */
 rwrt_status rwrt_rk45_run_tv_tails(rwrt_ctx* ctx, const rwrt_grid* g, const rwrt_background* b,
                                    int64_t nray, const rwrt_params* p,

@@ -887,6 +887,9 @@ struct CachedVaryingBG64 {
   unsigned lane16;
   mutable unsigned key_x, key_y;
   mutable int key_j;
+#ifdef RWRT_TV_MISS_DIAG
+  mutable unsigned misses = 0;   // (diagnostic build: refills made by this lane)
+#endif
 
   struct Pending {
     double w[4];
@@ -905,6 +908,9 @@ struct CachedVaryingBG64 {
     const double* A = V.level(t, p.wt, jl);
     p.B = A + (V.nlev > 1 ? V.lev_stride : 0);
     if (kx != key_x || ky != key_y || jl != key_j) {   // miss: refill by LDS-DMA
+#ifdef RWRT_TV_MISS_DIAG
+      ++misses;
+#endif
       char* const base = lds_slice_base(wave_base);
 #pragma unroll
       for (int j = 0; j < 4; ++j)
@@ -980,6 +986,114 @@ __device__ __forceinline__ CachedVaryingBG64::Pending lookup_begin(const CachedV
 }
 __device__ __forceinline__ void lookup_end(const CachedVaryingBG64& B,
                                            const CachedVaryingBG64::Pending& p, double g[11]) {
+  B.end(p, g);
+}
+
+// Latency mode of the time-varying ray loops (rk45_run_kernel's first
+// heavy_blocks blocks, run_rays<.., kReplica>): ONE ray per wavefront,
+// replicated on all 64 lanes (the same state and the same operations on every
+// lane, so the wave never diverges), whose lookups read a block of kP x kP
+// grid points (kP - 1 cells a side) of BOTH bracketing levels held in the
+// wave's 24 KiB of LDS.  The per-lane cell cache refills whenever a stage
+// leaves its cell or level pair -- 1.7-2.3 refills per attempt of the
+// heaviest C5 rays at 0.25 degrees (tools/c5_misses.py,
+// profiles/r5/c5lat/misses.json), each an HBM round trip in a dependent
+// chain; here a ray moves kP / 2 - 1 cells or more before the block is
+// reloaded, and a reload is kLoads wave-wide LDS-DMA instructions (64 lanes x
+// 16 B each) instead of 48 single-lane ones.  Records are contiguous in the
+// block: level lv, point (i, j) at ((lv * kP + i) * kP + j) * kRec bytes.  The
+// corner values are the level arrays' own (the same doubles or floats), the
+// blends and the time interpolation those of VaryingBG<T>::interp11: results
+// are the run kernel's bit for bit.
+template <class T>
+struct BlockVaryingBG {
+  static constexpr bool kTimeVarying = true;
+  static constexpr int kP = 8;                                  // grid points per side
+  static constexpr int kRec = 12 * (int)sizeof(T);              // one record: 96 B (fp64) / 48 B (fp32)
+  static constexpr int kCh = kRec / 16;                         // 16-B chunks per record
+  static constexpr int kChunks = 2 * kP * kP * kCh;             // chunks of a reload
+  static constexpr int kLoads = (kChunks + 63) / 64;            // wave-wide LDS-DMA instructions
+  static_assert(kChunks * 16 <= kCacheBytesPerWave, "block must fit the wave's LDS");
+  VaryingBG<T> V;
+  char* wave_base;
+  mutable int bx, by, bj;   // block origin (grid point) and level pair held (bj = -1: none)
+
+  struct Pending {
+    double w[4];
+    double wt;
+    unsigned o[4];   // LDS byte offsets of corners a, b, c, d in level A's block
+  };
+  __device__ __forceinline__ Pending begin(double lon, double lat, double t) const {
+    Pending p;
+    unsigned og[4], kx, ky;
+    int jl;
+    V.cell(lon, lat, og, p.w, kx, ky);
+    const T* A = V.level(t, p.wt, jl);
+    const int x0 = (int)(kx & 0xffffu), x1 = (int)(kx >> 16), y0 = (int)(ky & 0xffffu), y1 = (int)(ky >> 16);
+    if (!(jl == bj && x0 >= bx && x1 < bx + kP && y0 >= by && y1 < by + kP)) {
+      // reload (wave-uniform: every lane holds the same ray): the cell near
+      // the block's centre, the block inside the grid where it fits
+      bx = min(max(x0 - (kP / 2 - 1), 0), max(V.W - kP, 0));
+      by = min(max(y0 - (kP / 2 - 1), 0), max(V.H - kP, 0));
+      bj = jl;
+      const T* L[2] = {A, A + (V.nlev > 1 ? V.lev_stride : 0)};
+      char* const base = lds_slice_base(wave_base);
+      const int lane = (int)(threadIdx.x & 63u);
+#pragma unroll
+      for (int k = 0; k < kLoads; ++k) {
+        const int c = k * 64 + lane;   // chunk q of record r = (lv, i, j)
+        if (kChunks % 64 == 0 || c < kChunks) {
+          const int r = c / kCh, q = c - r * kCh;
+          const int lv = r / (kP * kP), pt = r - lv * (kP * kP);
+          const int i = pt / kP, j = pt - i * kP;
+          const int gx = min(bx + i, V.W - 1), gy = min(by + j, V.H - 1);
+          const T* src = L[lv] + (size_t)__umul24(__umul24(gx, V.H) + gy, kNF) + q * (16 / (int)sizeof(T));
+          __builtin_amdgcn_global_load_lds((global_void_ptr)src, (lds_void_ptr)(base + k * 1024), 16, 0, 0);
+        }
+      }
+    }
+    const unsigned xa = (unsigned)(x0 - bx), xb = (unsigned)(x1 - bx), ya = (unsigned)(y0 - by),
+                   yb = (unsigned)(y1 - by);
+    p.o[0] = (xa * kP + yb) * kRec;   // a = F[x0, y1]
+    p.o[1] = (xb * kP + yb) * kRec;   // b = F[x1, y1]
+    p.o[2] = (xa * kP + ya) * kRec;   // c = F[x0, y0]
+    p.o[3] = (xb * kP + ya) * kRec;   // d = F[x1, y0]
+    return p;
+  }
+  __device__ __forceinline__ double el(unsigned off, int f) const {
+    return (double)*reinterpret_cast<const T*>(wave_base + off + f * (int)sizeof(T));
+  }
+  __device__ __forceinline__ void end(const Pending& p, double g[11]) const {
+    lds_dma_wait();
+    double ga[11], gb[11];
+    constexpr unsigned kLev = kP * kP * kRec;
+#pragma unroll
+    for (int f = 0; f < 11; ++f)
+      ga[f] = VaryingBG<T>::bl(p.w, el(p.o[0], f), el(p.o[1], f), el(p.o[2], f), el(p.o[3], f));
+#pragma unroll
+    for (int f = 0; f < 11; ++f)
+      gb[f] = VaryingBG<T>::bl(p.w, el(p.o[0] + kLev, f), el(p.o[1] + kLev, f), el(p.o[2] + kLev, f),
+                               el(p.o[3] + kLev, f));
+#pragma unroll
+    for (int i = 0; i < 11; ++i) g[i] = ga[i] * (1.0 - p.wt) + gb[i] * p.wt;
+  }
+  __device__ __forceinline__ void interp4(double lon, double lat, double t, double& fu, double& fv,
+                                          double& fqx, double& fqy) const {
+    V.interp4(lon, lat, t, fu, fv, fqx, fqy);
+  }
+  __device__ static BlockVaryingBG make(const VaryingBG<T>& B, char* lds) {
+    const unsigned wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    return BlockVaryingBG{B, lds + wave * kCacheBytesPerWave, 0, 0, -1};
+  }
+};
+template <class T>
+__device__ __forceinline__ typename BlockVaryingBG<T>::Pending lookup_begin(const BlockVaryingBG<T>& B, double lon,
+                                                                            double lat, double t) {
+  return B.begin(lon, lat, t);
+}
+template <class T>
+__device__ __forceinline__ void lookup_end(const BlockVaryingBG<T>& B, const typename BlockVaryingBG<T>::Pending& p,
+                                           double g[11]) {
   B.end(p, g);
 }
 
@@ -2695,31 +2809,25 @@ using KStore = KShared<5>;
 #ifndef RWRT_RUN_ALIGN
 #define RWRT_RUN_ALIGN 256
 #endif
-template <class BG, bool kTrace = false>
-__global__ void __launch_bounds__(256, RunWaves<BG>::kPerSimd) __attribute__((aligned(RWRT_RUN_ALIGN)))
-rk45_run_kernel(RunArgs<BG> a) {
-  nm_stage<NM_ALL>();
-  using LBG = typename LaneBG<BG>::type;
+// the latency mode's background of a time-varying run kernel (none: void)
+template <class BG>
+struct TvBlock {
+  using type = void;
+};
+template <class T>
+struct TvBlock<VaryingBG<T>> {
+  using type = BlockVaryingBG<T>;
+};
+
+// The ray loop of rk45_run_kernel's blocks: each lane pulls rays from the
+// work queue (hw = -1), or -- kReplica, the time-varying latency mode -- every
+// lane of the wave runs the ray at order position hw, replicated, through a
+// BlockVaryingBG, and lane 0 stores its rows and state.
+template <class BG, class LBG, bool kTrace, bool kReplica>
+__device__ __forceinline__ void run_rays(const RunArgs<BG>& a, const LBG& lbg, char* smem, int64_t hw) {
   using RayProblem = RayProblemT<LBG>;
-  // all LDS in one array: the stages (5 x 5 doubles per lane) then the lookup cache
-  constexpr int kKBytes = 5 * 5 * 256 * 8;
-  __shared__ __attribute__((aligned(16))) char smem[kKBytes + LaneBG<BG>::kLdsBytes];
-  if constexpr (std::is_same<BG, StaticBG>::value) {
-    const int lb = (int)blockIdx.x;   // (latency block index)
-#ifdef RWRT_ANALYZE_QUAD
-    if (true) {   // (analysis build of the latency mode: its loop is the common path)
-#else
-    if (RARE(lb < a.heavy_blocks)) {   // (block-uniform) latency mode
-#endif
-      __builtin_amdgcn_s_setprio(1);
-      quad_rays<kTrace>(a, smem + kKBytes, reinterpret_cast<double*>(smem), lb);
-      return;
-    }
-  }
-  if constexpr (std::is_same<BG, VaryingBG<double>>::value) {
-    if (a.B.half && (threadIdx.x & 63u) >= 32u) return;   // half density: lanes 32-63's LDS slots hold the upper level
-  }
-  const RayProblem P{LaneBG<BG>::make(a.B, smem + kKBytes)};
+  const RayProblem P{lbg};
+  const bool writer = !kReplica || (threadIdx.x & 63u) == 0;   // (a latency wave's lane 0 stores)
   const int64_t nrows = a.it_end - a.it_begin;
   Lane<RayProblem, KStore> L;
   L.K.p = reinterpret_cast<double*>(smem) + threadIdx.x;
@@ -2727,12 +2835,22 @@ rk45_run_kernel(RunArgs<BG> a) {
   int64_t ray = -1, nacc = 0, nrej = 0;
   int32_t it = 0, nanrow = 0, wpos = 0;   // (wpos: the ray's queue position, kTrace only)
   double prev_lon = 0.0, prev_lat = 0.0, cos_prev = 0.0;
+#ifdef RWRT_TV_MISS_DIAG
+  unsigned miss0 = 0;   // (diagnostic build: trace[ray] += the ray's refills, time-varying fp64)
+#endif
   // above frozen_fill_kernel's waves (priority 0) sharing the SIMD: the
   // fill takes the issue cycles the ray loop leaves idle
   __builtin_amdgcn_s_setprio(1);
   for (;;) {
     if (ray < 0) {
-      const int64_t w = a.n_heavy + atomicAdd(&a.queue[1], 1);
+      int64_t w;
+      if (kReplica) {   // a latency wave: its one ray, then done
+        if (hw < 0) break;
+        w = hw;
+        hw = -1;
+      } else {
+        w = a.n_heavy + atomicAdd(&a.queue[1], 1);
+      }
       if (w >= a.nray) break;
       ray = a.order ? a.order[w] : w;
       if (kTrace) {
@@ -2757,6 +2875,9 @@ rk45_run_kernel(RunArgs<BG> a) {
       nrej = a.count[2 * ray + 1];
       nanrow = a.nanrow[ray];
       it = a.it_begin;
+#ifdef RWRT_TV_MISS_DIAG
+      if constexpr (std::is_same<LBG, CachedVaryingBG64>::value) miss0 = P.B.misses;
+#endif
       prev_lon = L.y[0];   // == rlon[it-1], rlat[it-1] (wr.py:844, 877-885)
       prev_lat = L.y[1];
       cos_prev = k_cos(prev_lat);
@@ -2800,7 +2921,7 @@ rk45_run_kernel(RunArgs<BG> a) {
     // masks against itself is a no-op), so every remaining row of the chunk
     // equals this one: write them all and release the lane.
     const int last = (st == Lane<RayProblem, KStore>::kFrozen) ? a.it_end : it + 1;
-    {
+    if (writer) {
       // non-temporal, like the fill's: the rows stream past the L2 that
       // holds the basic state (+0.5 % on C3, profiles/r3/sched/pass_aa_nt_rows.txt;
       // no row stores at all would be +3.3 %)
@@ -2810,7 +2931,7 @@ rk45_run_kernel(RunArgs<BG> a) {
       store_row16<RWRT_ROW_NT>(o + 2, r2);
       store_row16<RWRT_ROW_NT>(o + 3, r3);
     }
-    if (RARE(last > it + 1)) {
+    if (RARE(last > it + 1) && writer) {
       asm volatile("");   // frozen: the remaining rows of the chunk (rare branch)
       for (int k = it + 1; k < last; ++k) {
         double2* o = reinterpret_cast<double2*>(a.out + ((size_t)ray * nrows + (k - a.it_begin)) * RWRT_NOUT);
@@ -2826,7 +2947,7 @@ rk45_run_kernel(RunArgs<BG> a) {
     cos_prev = cos_c;
     it = last;
     if (st == Lane<RayProblem, KStore>::kFrozen) L.t = a.tbound[a.it_end - 1];
-    if (it == a.it_end) {
+    if (it == a.it_end && writer) {
 #pragma unroll
       for (int v = 0; v < 5; ++v) {
         a.state[v * a.nray + ray] = y[v];
@@ -2839,9 +2960,51 @@ rk45_run_kernel(RunArgs<BG> a) {
       a.count[2 * ray] = nacc;
       a.count[2 * ray + 1] = nrej;
       a.nanrow[ray] = nanrow;
+#ifdef RWRT_TV_MISS_DIAG
+      if constexpr (std::is_same<LBG, CachedVaryingBG64>::value)
+        if (a.trace && ray < a.trace_cap) a.trace[ray] += (int64_t)(P.B.misses - miss0);
+#endif
       ray = -1;
     }
+    if (kReplica && it == a.it_end) ray = -1;   // (the other lanes of a latency wave)
   }
+}
+
+template <class BG, bool kTrace = false>
+__global__ void __launch_bounds__(256, RunWaves<BG>::kPerSimd) __attribute__((aligned(RWRT_RUN_ALIGN)))
+rk45_run_kernel(RunArgs<BG> a) {
+  nm_stage<NM_ALL>();
+  // all LDS in one array: the stages (5 x 5 doubles per lane) then the lookup cache
+  constexpr int kKBytes = 5 * 5 * 256 * 8;
+  __shared__ __attribute__((aligned(16))) char smem[kKBytes + LaneBG<BG>::kLdsBytes];
+  if constexpr (std::is_same<BG, StaticBG>::value) {
+    const int lb = (int)blockIdx.x;   // (latency block index)
+#ifdef RWRT_ANALYZE_QUAD
+    if (true) {   // (analysis build of the latency mode: its loop is the common path)
+#else
+    if (RARE(lb < a.heavy_blocks)) {   // (block-uniform) latency mode
+#endif
+      __builtin_amdgcn_s_setprio(1);
+      quad_rays<kTrace>(a, smem + kKBytes, reinterpret_cast<double*>(smem), lb);
+      return;
+    }
+  }
+  if constexpr (!std::is_void<typename TvBlock<BG>::type>::value) {
+    // latency mode of the time-varying loops: blocks [0, heavy_blocks) run
+    // order[0, n_heavy), one ray per wave replicated on its 64 lanes
+    // (BlockVaryingBG), consecutive positions on consecutive waves
+    if (RARE((int)blockIdx.x < a.heavy_blocks)) {   // (block-uniform)
+      const int64_t w = (int64_t)blockIdx.x * 4 + (int64_t)(threadIdx.x >> 6);
+      if (w >= a.n_heavy) return;
+      using BBG = typename TvBlock<BG>::type;
+      run_rays<BG, BBG, false, true>(a, BBG::make(a.B, smem + kKBytes), smem, w);
+      return;
+    }
+  }
+  if constexpr (std::is_same<BG, VaryingBG<double>>::value) {
+    if (a.B.half && (threadIdx.x & 63u) >= 32u) return;   // half density: lanes 32-63's LDS slots hold the upper level
+  }
+  run_rays<BG, typename LaneBG<BG>::type, kTrace, false>(a, LaneBG<BG>::make(a.B, smem + kKBytes), smem, -1);
 }
 
 // ---------------------------------------------------------------------------
@@ -3551,17 +3714,22 @@ rwrt_status launch_run(rwrt_ctx* ctx, const BG& B, int64_t nray, const rwrt_para
   if (nray == 0) return RWRT_OK;
   if (n_heavy < 0 || n_heavy > nray) return fail(RWRT_ERR_ARG, "n_heavy out of range%s");
   if (n_heavy > 0 && !d_order) return fail(RWRT_ERR_ARG, "n_heavy > 0 needs d_order%s");
-  if (n_heavy > 0 && !std::is_same<BG, StaticBG>::value)
-    return fail(RWRT_ERR_ARG, "latency mode (n_heavy > 0) runs on the static background only%s");
+  // (latency mode: quad_rays on the static background, replicated waves with
+  // a block cache on the time-varying ones -- rk45_run_kernel's first
+  // heavy_blocks blocks either way; none for the fp32-arithmetic variant)
+  if (n_heavy > 0 && std::is_void<typename TvBlock<BG>::type>::value && !std::is_same<BG, StaticBG>::value)
+    return fail(RWRT_ERR_ARG, "latency mode (n_heavy > 0) is not built for fp32-arithmetic levels%s");
   // the context's settings are read once, under its lock: a concurrent
   // rwrt_ctx_set_latency_density cannot change the density between sizing the
   // latency-mode grid and launching it
   std::lock_guard<std::mutex> lock(ctx->mu);
   const int32_t quad_per_wave = ctx->quad_per_wave;
-  const int64_t per_block = 4 * (int64_t)quad_per_wave;   // rays per latency-mode block
+  // rays per latency-mode block: quad_rays 4 x rays-per-wave, the
+  // time-varying latency waves one ray per wave
+  const int64_t per_block = BG::kTimeVarying ? 4 : 4 * (int64_t)quad_per_wave;
   const int64_t team_blocks = (n_heavy + per_block - 1) / per_block;
   if (team_blocks > ctx->ncu / 2)
-    return fail(RWRT_ERR_ARG, "n_heavy exceeds the latency mode's capacity (4 x rays-per-wave per CU, half the CUs)%s");
+    return fail(RWRT_ERR_ARG, "n_heavy exceeds the latency mode's capacity (per CU 4 x rays-per-wave, time-varying 4; half the CUs)%s");
   DeviceGuard dg(ctx->device);
   if (!dg.ok) return check_launch("hipSetDevice(context device)");
   hipStream_t st = (hipStream_t)stream;
@@ -3603,9 +3771,15 @@ rwrt_status launch_run(rwrt_ctx* ctx, const BG& B, int64_t nray, const rwrt_para
     a.trace = ctx->trace;
     a.trace_cap = ctx->trace ? ctx->trace_cap : 0;
   }
+#ifdef RWRT_TV_MISS_DIAG
+  if constexpr (std::is_same<BG, VaryingBG<double>>::value) {   // (per-ray refill counts, indexed by ray)
+    a.trace = ctx->trace;
+    a.trace_cap = ctx->trace ? ctx->trace_cap : 0;
+  }
+#endif
   if (nray > n_heavy || team_blocks) {
     const int64_t grid = team_blocks + (nray > n_heavy ? blocks : 0);
-    if (a.trace) {
+    if (a.trace && std::is_same<BG, StaticBG>::value) {
       if constexpr (std::is_same<BG, StaticBG>::value)
         hipLaunchKernelGGL((rk45_run_kernel<BG, true>), dim3((unsigned)grid), dim3(256), 0, st, a);
     } else {

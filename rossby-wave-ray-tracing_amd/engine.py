@@ -115,6 +115,7 @@ class RayEngine:
     bg = None   # rwrt_background of a time-varying state (None: the reference's static state)
     split_rho = None   # the last advance()'s rank correlation of its leading launches (split="auto")
     launch_log = ()    # the last advance()'s launches: rows and latency-mode decision
+    keep_launch_work = False   # diagnostics: launch_work = [(attempts per ray, latency set)] per launch
     _ctx = None
 
     @property
@@ -318,14 +319,16 @@ class RayEngine:
 
     CELL_PER_OCTAVE = int(os.environ.get("RWRT_CELL_PER_OCTAVE", "2"))   # (env: A/B only)
 
-    def cost_cell_order(self, st, work, per_octave=None):
+    def cost_cell_order(self, st, work, per_octave=None, head=0):
         """``cost_order`` with spatial locality: rays in coarse cost classes
         (``per_octave`` classes per doubling of the previous launch's work,
         heaviest class first) and, within a class, in Morton order of their
         current grid cell, so that the 64 rays a wave starts with share cache
         lines and L2 / MALL sets in their first lookups (the 0.25-degree
         time-varying state of C5 is gathered from HBM: 100 MB per fp64
-        level).  Frozen rays last."""
+        level).  Frozen rays last.  ``head``: the ``head`` heaviest live rays
+        by ``work`` go first, longest first (the latency mode takes its rays
+        from the order's head; a cost class alone does not rank them)."""
         per_octave = self.CELL_PER_OCTAVE if per_octave is None else per_octave
         y = st["state"][:5]
         frozen = torch.isnan(y.sum(0))
@@ -337,7 +340,15 @@ class RayEngine:
         iy = torch.floor((y[1] - g.lat0) / g.dlat).nan_to_num(0).clamp(0, g.nrow - 1).to(torch.int64)
         key = cls * (1 << 32) + ((1 << 32) - 1 - morton2(ix, iy))
         key = torch.where(frozen, torch.full_like(key, -1), key)
-        return torch.sort(key, descending=True, stable=True).indices.to(torch.int64).contiguous()
+        order = torch.sort(key, descending=True, stable=True).indices.to(torch.int64)
+        if head:
+            kw = torch.where(frozen, torch.full_like(work, -1), work)
+            top = torch.topk(kw, min(int(head), kw.numel())).indices
+            top = top[kw[top] >= 0]
+            first = torch.zeros(kw.numel(), dtype=torch.bool, device=kw.device)
+            first[top] = True
+            order = torch.cat([top.to(torch.int64), order[~first[order]]])
+        return order.contiguous()
 
     # a heavy ray's attempt in latency mode / in a loaded rk45_run_kernel wave
     # (round 2, tools/team_latency.py on the heaviest C3 rays: 10.2 us alone in
@@ -353,6 +364,13 @@ class RayEngine:
     # 0.56 s at 1 per wave, 256 rays 0.27 s at 4 per wave), so only 16
     # (RWRT_QUAD_DENSITIES=4,16 lets the rule consider others: A/B only)
     QUAD_DENSITIES = tuple(int(x) for x in os.environ.get("RWRT_QUAD_DENSITIES", "16").split(","))
+    # the time-varying latency waves (one ray per wave, BlockVaryingBG): a heavy
+    # C5 ray's attempt there against a loaded run-kernel lane's
+    TV_RATIO = float(os.environ.get("RWRT_TV_RATIO", "0.77"))
+
+    def team_capacity_tv(self):
+        """Rays the time-varying latency mode takes at most (4 per CU, half the CUs)."""
+        return (torch.cuda.get_device_properties(self.device).multi_processor_count // 2) * 4
 
     def team_capacity(self):
         """Rays the latency mode takes at most (64 per CU, half the CUs)."""
@@ -365,14 +383,15 @@ class RayEngine:
         ``(n, rays_per_wave)`` for both; "auto"
         picks the pair that minimises the launch's predicted makespan from each
         ray's previous-launch work (below)."""
-        if order is None or self.bg is not None:   # (the latency mode is static-background only)
+        if order is None or (self.bg is not None and self.bg.fp32 == 2):   # (none for fp32 arithmetic)
             return 0, 16
         live = ~torch.isnan(st["state"][:5].sum(0))
         n_live = int(live.sum().item())
         ncu = torch.cuda.get_device_properties(self.device).multi_processor_count
         if team != "auto":
             n, q = (int(team[0]), int(team[1])) if isinstance(team, (tuple, list)) else (int(team), 16)
-            n = min(n, (ncu // 2) * 4 * q, n_live)
+            # (time-varying: one ray per latency wave, 4 per CU)
+            n = min(n, (ncu // 2) * 4 * (1 if self.bg is not None else q), n_live)
             # the first n entries of the order must be live rays
             return (n if n == 0 or bool(live[order[:n]].all()) else 0), q
         if work is None or n_live < 1:
@@ -386,14 +405,17 @@ class RayEngine:
         w = torch.where(live, work, torch.zeros_like(work))[order].to(torch.float64)
         cum = torch.cumsum(w, 0)
         best = None
-        for q in self.QUAD_DENSITIES:
+        tv = self.bg is not None   # (time-varying: one ray per latency wave; 32 or 64 run lanes per wave)
+        lanes_cu = (4.0 * self.tv_lanes) if tv else 256.0
+        for q in ((1,) if tv else self.QUAD_DENSITIES):
             cap = min((ncu // 2) * 4 * q, n_live)
             n = torch.arange(0, cap + 1, 4 * q, device=w.device)
             n = torch.unique(torch.cat([n, torch.tensor([cap], device=w.device)]))
             rest = cum[-1] - torch.where(n > 0, cum[(n - 1).clamp(min=0)], torch.zeros_like(cum[:1]))
-            lanes = 256.0 * (ncu - (n + 4 * q - 1) // (4 * q)).clamp(min=1)
+            lanes = lanes_cu * (ncu - (n + 4 * q - 1) // (4 * q)).clamp(min=1)
             nxt = torch.where(n < w.numel(), w[n.clamp(max=w.numel() - 1)], torch.zeros_like(rest))
-            ratio = self.QUAD_RATIO_1 + (self.QUAD_RATIO_16 - self.QUAD_RATIO_1) * (q - 1) / 15.0
+            ratio = self.TV_RATIO if tv else \
+                self.QUAD_RATIO_1 + (self.QUAD_RATIO_16 - self.QUAD_RATIO_1) * (q - 1) / 15.0
             t = torch.maximum(torch.maximum(nxt, rest / lanes),
                               torch.where(n > 0, w[0] * ratio, torch.zeros_like(rest)))
             k = int(torch.argmin(t).item())
@@ -619,6 +641,7 @@ class RayEngine:
         self.split_rho = None
         auto_split, split_rows = self.parse_split(split)   # (cuts of the long launch)
         self.launch_log = []   # per launch: rows, rays in latency mode (diagnostics)
+        self.launch_work = []
         k = 0
         while k < len(bounds):
             i0, i1 = bounds[k]
@@ -640,9 +663,11 @@ class RayEngine:
             if order_policy in ("cost", "priority", "cell", "total") and prev_work is not None:
                 # the previous launch's attempts per ray, or ("total") all of them so far
                 work = cnt.sum(1) - (0 if order_policy == "total" else prev_work)
-                order = self.cost_cell_order(st, work) if order_policy == "cell" else self.cost_order(st, work)
             # (a list: one latency-mode size per launch, the last repeated)
             tk = team[min(k, len(team) - 1)] if isinstance(team, list) else team
+            if order_policy in ("cost", "priority", "cell", "total") and prev_work is not None:
+                order = (self.cost_cell_order(st, work, head=self.team_capacity_tv() if tk else 0)
+                         if order_policy == "cell" else self.cost_order(st, work))
             n_heavy, qpw = self.team_size(tk, st, work, order, i1 - i0) if tk else (0, 16)
             self.launch_log.append({"rows": [int(i0), int(i1)], "n_heavy": int(n_heavy), "per_wave": int(qpw)})
             if os.environ.get("RWRT_DEBUG_TEAM"):
@@ -658,6 +683,8 @@ class RayEngine:
                 self.run(st, p, tb, i0, i1, view, order, n_heavy, qpw, tails)
             if auto_split and k < n_lead:
                 works = (works + [cnt.sum(1) - prev_work])[-2:]
+            if self.keep_launch_work:   # (diagnostics: each launch's attempts per ray and its latency set)
+                self.launch_work.append((cnt.sum(1) - prev_work, order[:n_heavy].clone() if n_heavy else None))
             if sink is not None:
                 deliver(self, sink, i0, i1, view, tails)
             elif tails is not None and out is not None:

@@ -230,6 +230,49 @@ def cost_partition(cost, frozen, rank, world):
     return torch.sort(order[owner == rank]).values
 
 
+def probe_share(nray, rank, world, device):
+    """The rays ``rank`` probes when the probe is sharded: every ``world``-th
+    slot from ``rank`` (interleaved, so each share holds every kind of ray)."""
+    return torch.arange(rank, nray, world, device=device, dtype=torch.int64)
+
+
+def probe_costs(eng, st, p, tb, npr, rank, world, group=None):
+    """Each ray's probe cost, the probe sharded: this rank runs rows [1, 1 +
+    npr) for its ``probe_share`` of the rays (from the initial state ``st``,
+    which stays untouched) and the per-ray results are all-gathered -- ONE
+    collective of 8 B per ray (RCCL over xGMI: 19 MB for C3, 77 MB for C5) --
+    into ``(cost, frozen)`` over every ray, the same on every rank.  Without a
+    group (a single-GPU rehearsal of one rank) every share is probed here.
+    A ray's probe is the same on any rank (rays are independent), so the costs
+    equal the unsharded probe's bit for bit."""
+    nray = st["nray"]
+    dev = st["state"].device
+    m = -(-nray // world)
+
+    def one(r):
+        sh = probe_share(nray, r, world, dev)
+        sub = eng.take(st, sh)
+        rows = torch.empty((sh.numel(), npr, 8), dtype=torch.float64, device=dev)
+        eng.run(sub, p, tb, 1, 1 + npr, rows, eng.live_first_order_of(sub), 0, tails=eng.tails(sh.numel()))
+        v = torch.where(torch.isnan(sub["state"][:5].sum(0)), torch.full_like(sub["count"][:, 0], -1),
+                        sub["count"].sum(1))
+        out = torch.full((m,), -2, dtype=torch.int64, device=dev)
+        out[: v.numel()] = v
+        return out
+    if group is not None and world > 1:
+        mine = one(rank)
+        cdev = _dev(group)
+        parts = [torch.empty(m, dtype=torch.int64, device=cdev) for _ in range(world)]
+        dist.all_gather(parts, mine.to(cdev), group=group)
+        parts = [x.to(dev) for x in parts]
+    else:
+        parts = [one(r) for r in range(world)]
+    v = torch.empty(nray, dtype=torch.int64, device=dev)
+    for r, x in enumerate(parts):
+        v[r::world] = x[: len(range(r, nray, world))]
+    return v.clamp(min=0), v < 0
+
+
 class ShardedRun:
     """Outcome of ``run_sharded`` on one rank."""
 
@@ -244,7 +287,8 @@ class ShardedRun:
 
 def run_sharded(eng, y0, nt, tstep=7200.0, group=None, rank=None, world=None, probe=6,
                 lead=(24, 96), chunk=None, out=None, sink=None, events=None, gather=True,
-                ttotal=None, order_policy="priority", team=0, split=None):
+                ttotal=None, order_policy="priority", team=0, split=None, shard_probe=False,
+                costs=None):
     """One ray set ``y0[5, nray]`` (identical on every rank) integrated across
     the ranks of ``group``.
 
@@ -256,6 +300,12 @@ def run_sharded(eng, y0, nt, tstep=7200.0, group=None, rank=None, world=None, pr
     tensors).  ``sink(i0, i1, rows, idx)`` receives this rank's rows.
     ``team`` is ``RayEngine.advance``'s latency-mode size per launch, ``split``
     its adaptive split of the long launch.
+    ``shard_probe`` (world > 1): each rank probes only its ``probe_share``
+    and the probe costs are all-gathered (``probe_costs``); the rank then
+    re-runs the probe rows for its own shard only -- 2/world of the probe's
+    work per rank instead of all of it.  ``costs`` (rehearsals): the
+    ``(cost, frozen)`` of ``probe_costs`` computed beforehand, so that the
+    timed call runs only this rank's share.
     ``rank``/``world`` without a group emulate one rank of a larger job on
     this device (single-GPU rehearsal: no collectives).  Rays are independent
     and both global couplings are decided over every ray, so the union of the
@@ -273,18 +323,39 @@ def run_sharded(eng, y0, nt, tstep=7200.0, group=None, rank=None, world=None, pr
     if int(summary[0]) > 0 and int(summary[1]) == 0:      # rkf45.py:423-425 (all rays, every rank)
         return ShardedRun(None, None, 0, failed=True)
     npr = min(probe, nt - 1)
-    prow = torch.empty((nray, npr, 8), dtype=torch.float64, device=eng.device)
-    ptails = eng.tails(nray)
     if events is not None:
         e0, e1, es = eng._event_pair()
-    eng.run(st, p, tb, 1, 1 + npr, prow, eng.live_first_order_of(st), 0, tails=ptails)
-    if events is not None:
-        e1.record(es)
-        events.append((e0, e1))
-    cost = st["count"].sum(1)                        # attempts in the probe
-    frozen = torch.isnan(st["state"][:5].sum(0))
-    idx = cost_partition(cost, frozen, rank, world)
-    local = eng.take(st, idx)
+    if world > 1 and (shard_probe or costs is not None):
+        if costs is None:
+            cost, frozen = probe_costs(eng, st, p, tb, npr, rank, world, group=group)
+        else:   # (a rehearsal: the other shares were probed beforehand)
+            cost, frozen = costs
+            sh = probe_share(nray, rank, world, eng.device)
+            sub = eng.take(st, sh)
+            eng.run(sub, p, tb, 1, 1 + npr, torch.empty((sh.numel(), npr, 8), dtype=torch.float64,
+                                                         device=eng.device),
+                    eng.live_first_order_of(sub), 0, tails=eng.tails(sh.numel()))
+        idx = cost_partition(cost, frozen, rank, world)
+        local = eng.take(st, idx)                    # (the initial state: re-probe this shard)
+        prow = torch.empty((idx.numel(), npr, 8), dtype=torch.float64, device=eng.device)
+        ptails = eng.tails(idx.numel())
+        eng.run(local, p, tb, 1, 1 + npr, prow, eng.live_first_order_of(local), 0, tails=ptails)
+        prow_local, ptails_local = prow, ptails
+        if events is not None:
+            e1.record(es)
+            events.append((e0, e1))
+    else:
+        prow = torch.empty((nray, npr, 8), dtype=torch.float64, device=eng.device)
+        ptails = eng.tails(nray)
+        eng.run(st, p, tb, 1, 1 + npr, prow, eng.live_first_order_of(st), 0, tails=ptails)
+        if events is not None:
+            e1.record(es)
+            events.append((e0, e1))
+        cost = st["count"].sum(1)                        # attempts in the probe
+        frozen = torch.isnan(st["state"][:5].sum(0))
+        idx = cost_partition(cost, frozen, rank, world)
+        local = eng.take(st, idx)
+        prow_local, ptails_local = prow[idx], None if ptails is None else ptails.take(idx)
     last = {}
 
     def keep(i0, i1, rows, tails=None):
@@ -300,7 +371,7 @@ def run_sharded(eng, y0, nt, tstep=7200.0, group=None, rank=None, world=None, pr
             sink(i0, i1, rows, idx)
     keep.takes_tails = True
 
-    keep(1, 1 + npr, prow[idx], None if ptails is None else ptails.take(idx))
+    keep(1, 1 + npr, prow_local, ptails_local)
     n_live_local = int((~frozen[idx]).sum().item())
     res = eng.advance(local, p, tb, 1 + npr, chunk=chunk, sink=keep, out=out, events=events,
                       group=group, order_policy=order_policy, first_chunk=list(lead),

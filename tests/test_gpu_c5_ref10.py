@@ -124,7 +124,7 @@ def _c5_worker(rank, world, port, storage, q):
         parts = []
         r = run_sharded(eng, r0[:5].contiguous(), nt, 7200.0, group=dist.group.WORLD, probe=6, lead=[24, 96],
                         chunk=c5_rows_per_launch(storage == "fp32", world, nt), ttotal=(nt - 1) * 7200.0,
-                        order_policy="cell",
+                        order_policy="cell", shard_probe=True,   # (bench.py's split: the probe sharded too)
                         sink=lambda a, b, o, idx: parts.append(o[:, :, :7].cpu()))
         mine = torch.cat(parts, dim=1)                                   # (n_local, nt-1, 7)
         full = gather_rows(mine, r.idx.cpu().numpy(), r0.shape[1], group=dist.group.WORLD)
@@ -177,3 +177,62 @@ def test_c5_world2_split_bitwise_with_oracle(storage):
     assert np.array_equal(got, g["row_sha"]), f"{int((got != g['row_sha']).sum())} of {nt} rows differ"
     assert np.array_equal(counts[:, 0], g["nacc"])
     assert np.array_equal(counts[:, 1], g["nrej"])
+
+
+# ------------------------------------- C5 latency waves (BlockVaryingBG)
+@pytest.mark.parametrize("storage,lanes", [("fp64", 32), ("fp64", 64), ("fp32", 64)])
+def test_c5_latency_waves_bitwise(storage, lanes):
+    """The time-varying latency mode (rk45_run_kernel's first blocks: one ray
+    per wave, replicated on its 64 lanes, lookups from a block of grid points
+    of both levels in LDS) is a schedule: the whole C5 set over 41 levels
+    (10 days) with the 512 heaviest rays of every launch in it must end with
+    every ray's last row and attempt counts equal, bit for bit, to the run
+    without it -- and, on the fixture's 4 096-ray sample, the oracle's rows."""
+    import torch
+    import synthetic as S
+    from engine import RayEngine
+    from levels import Levels
+    from shard import run_sharded
+    from bench import c5_rows_per_launch
+    g = golden(f"c5_ref10_{storage}.npz")
+    nt, nlev = int(g["nt"]), int(g["nlev"])
+    b0 = S.background_level(0, res=0.25)
+    lv = Levels(b0["lat"], b0["lon"], nlev, t0=0.0, dt=6 * 3600.0, fp32=storage == "fp32")
+    for j in range(nlev):
+        bj = b0 if j == 0 else S.background_level(j, res=0.25)
+        lv.set_level(j, bj["u"], bj["v"])
+    eng = RayEngine.from_levels(lv)
+    eng.tv_lanes = lanes
+    cfg = S.config("C5")
+    deg2rad = np.pi / 180.0
+    ix, iy = np.meshgrid(np.arange(cfg.nnx), np.arange(cfg.nny))
+    lon = ((cfg.SW_lon % 360.0 + ix.ravel() * cfg.dlon) % 360.0) * deg2rad
+    lat = (cfg.SW_lat + iy.ravel() * cfg.dlat) * deg2rad
+    src = eng.sources(lon, lat)
+    rows0 = torch.cat([eng.initial_rows_dev(src, eng.zwn_tensor(cfg.zwn, S.c3_freq(P)))[0].reshape(7, -1)
+                       for P in S.C3_PERIODS_DAYS], dim=1)
+    idx = torch.as_tensor(g["idx"], device=eng.device)
+    pos = torch.full((rows0.shape[1],), -1, dtype=torch.int64, device=eng.device)
+    pos[idx] = torch.arange(idx.numel(), device=eng.device)
+    chunk = c5_rows_per_launch(lv.fp32, 1, nt)
+    runs = {}
+    for team in (0, (512, 1)):
+        hist = np.full((7, nt, idx.numel()), np.nan)
+        hist[:, 0] = rows0[:, idx].cpu().numpy()
+
+        def sink(i0, i1, rows, ridx, hist=hist):
+            p = pos[ridx]
+            m = p >= 0
+            hist[:, i0:i1, p[m].cpu().numpy()] = np.transpose(rows[m][:, :, :7].cpu().numpy(), (2, 1, 0))
+        r = run_sharded(eng, rows0[:5].contiguous(), nt, 7200.0, rank=0, world=1, probe=6, lead=[24, 96],
+                        chunk=chunk, sink=sink, ttotal=(nt - 1) * 7200.0, order_policy="cell", team=team)
+        heavy = [d["n_heavy"] for d in eng.launch_log]
+        runs[team] = (r.endpoints.cpu().numpy(), r.counts.cpu().numpy(), hist, heavy)
+    (e0, c0, _, h0), (e1, c1, hist, h1) = runs[0], runs[(512, 1)]
+    del eng, lv
+    torch.cuda.empty_cache()
+    assert max(h0) == 0 and min(h1) == 512, (h0, h1)
+    assert np.array_equal(c1, c0)
+    same = (e1 == e0) | (np.isnan(e1) & np.isnan(e0))
+    assert same.all(), f"{int((~same).any(1).sum())} rays end differently"
+    assert np.array_equal(row_hashes(hist), g["row_sha"])

@@ -90,7 +90,7 @@ def _free_port():
     return p
 
 
-def _c4_worker(rank, world, port, q):
+def _c4_worker(rank, world, port, q, shard_probe=False):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     root = os.path.dirname(here)
@@ -111,7 +111,7 @@ def _c4_worker(rank, world, port, q):
         y0 = c3_initial_state(bs)[:, g["idx"]]
         nt = C3_DAYS * 12 + 1
         parts = []
-        r = run_sharded(eng, y0, nt, group=dist.group.WORLD, chunk=48,
+        r = run_sharded(eng, y0, nt, group=dist.group.WORLD, chunk=48, shard_probe=shard_probe,
                         sink=lambda a, b, o, idx: parts.append(o.cpu()))
         mine = torch.cat(parts, dim=1)                      # (n_local, nt-1, 8)
         full = gather_rows(mine, r.idx.cpu().numpy(), y0.shape[1], group=dist.group.WORLD)
@@ -127,13 +127,16 @@ def _c4_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_c4_cost_sharded_world2_equals_single_gpu():
+@pytest.mark.parametrize("shard_probe", [False, True])
+def test_c4_cost_sharded_world2_equals_single_gpu(shard_probe):
+    """``shard_probe``: each rank probes half the rays and the probe costs are
+    all-gathered (shard.probe_costs), then each re-probes its own shard."""
     import torch.multiprocessing as mp
     hist, nacc, y0, bg, nt = c3_run()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_c4_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_c4_worker, args=(r, 2, port, q, shard_probe)) for r in range(2)]
     for p in procs:
         p.start()
     msgs = [q.get(timeout=110) for _ in range(2)]

@@ -72,9 +72,16 @@ def test_explicit_sizes_and_frozen_heads(eng):
     # the order's head must be live rays
     st2 = state_of(5000, frozen=5000)
     assert eng.team_size(300, st2, w, order, 10) == (0, 16)
-    # no order (live-first launches) or a time-varying background: none
+    # no order (live-first launches): none
     assert eng.team_size("auto", st, w, None, 10) == (0, 16)
-    eng.bg = object()
+    # a time-varying background: one ray per latency wave, 4 per CU on half
+    # the CUs; none with fp32 arithmetic (rwrt_background.fp32 == 2)
+    import types
+    eng.bg, eng.tv_lanes = types.SimpleNamespace(fp32=0), 32
+    assert eng.team_size((10 ** 6, 1), st, w, order, 10) == (128 * 4, 1)
+    assert eng.team_size(300, st, w, order, 10)[0] == 300
+    eng.bg = types.SimpleNamespace(fp32=2)
+    assert eng.team_size(300, st, w, order, 10) == (0, 16)
     assert eng.team_size("auto", st, w, order, 10) == (0, 16)
 
 

@@ -79,6 +79,8 @@ def main():
     ap.add_argument("--fields", default="fp64", choices=["fp64", "fp32"], help="C5: level storage")
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--chunk", type=int, default=0, help="C5: rows per launch (default: bench.py's, 48 fp64 / 240 fp32)")
+    ap.add_argument("--shard-probe", type=int, default=1, choices=[0, 1],
+                    help="each rank probes 1/W of the rays, costs all-gathered (bench.py's default)")
     a = ap.parse_args()
     # 'auto', an int (rays per launch at 16 per wave) or n:q (n rays at q per wave)
     team = a.team if a.team == "auto" else (tuple(int(x) for x in a.team.split(":")) if ":" in a.team
@@ -89,7 +91,7 @@ def main():
     if a.config == "C5":
         eng, y0, _ = c5_setup(a, nt)
         kw = dict(order_policy="cell", ttotal=(nt - 1) * 7200.0)
-        team = 0
+        team = 0 if a.team == "auto" else team   # (C5: sparse-wave latency mode only when asked)
     else:
         bs, bg = bench.make_bs(a.bg)
         y0 = torch.as_tensor(bench.c3_initial_state(bs), device="cuda")
@@ -105,44 +107,74 @@ def main():
             n_local = -(-int(y0.shape[1]) // w) + 2
             cap = max(1, int(0.8 * torch.cuda.mem_get_info()[0]) // (n_local * 64))
             kw_w["chunk"] = min(a.chunk or bench.c5_rows_per_launch(a.fields == "fp32", w, nt), cap)
+        if w > 1 and a.shard_probe:   # every share's probe, untimed (the all-gather's result)
+            from engine import t_eval_of
+            from shard import probe_costs
+            p = eng.params(nt, 7200.0)
+            st0 = eng.init(y0, p)
+            tb = torch.as_tensor(t_eval_of(nt, 7200.0, kw.get("ttotal")), dtype=torch.float64, device=eng.device)
+            kw_w["costs"] = probe_costs(eng, st0, p, tb, 6, 0, w)
+            del st0
         for r in range(w):
             dt, res = timed(lambda: run_sharded(eng, y0, nt, rank=r, world=w, gather=False,
                                                        team=team, lead=lead, **kw_w), reps=a.reps)
             ev = []
+            eng.keep_launch_work = True
             run_sharded(eng, y0, nt, rank=r, world=w, gather=False, team=team, lead=lead, events=ev, **kw_w)
             torch.cuda.synchronize()
+            eng.keep_launch_work = False
+            # the last launch's heaviest rays: attempts there, and whether the
+            # latency set (chosen from the previous launch's work) held them
+            lw, lset = eng.launch_work[-1]
+            top = torch.topk(lw, 8)
+            inset = (torch.isin(top.indices, lset).tolist() if lset is not None else [False] * 8)
+            last_top = [[int(a_), bool(b_)] for a_, b_ in zip(top.values.tolist(), inset)]
             launches = [dict(d, ms=a_.elapsed_time(b_)) for d, (a_, b_) in
-                        zip([{"rows": [1, 1 + 6], "n_heavy": 0, "per_wave": 16}] + list(eng.launch_log), ev)]
+                        zip([{"rows": [1, 1 + 6], "n_heavy": 0, "per_wave": 16,
+                                               "probe": "share + own shard" if "costs" in kw_w else "every ray"}]
+                                             + list(eng.launch_log), ev)]
             att = (res.res.nacc + res.res.nrej)
             ranks.append({"rank": r, "s": dt, "rays": int(res.idx.numel()), "ray_steps": res.steps_local,
                           "max_attempts": int(att.max().item()),
                           "top_attempts": [int(x) for x in torch.topk(att, min(8, att.numel())).values.tolist()],
+                          "last_launch_top": last_top,
                           "launches": launches})
         steps = sum(x["ray_steps"] for x in ranks)
         mk = max(x["s"] for x in ranks)
         out["worlds"][str(w)] = {"makespan_s": mk, "rate": steps / mk, "ray_steps": steps,
-                                 "rows_per_launch": kw_w.get("chunk"), "ranks": ranks}
+                                 "rows_per_launch": kw_w.get("chunk"), "ranks": ranks,
+                                 "shard_probe": bool(w > 1 and a.shard_probe)}
         print(json.dumps({"world": w, "makespan_s": mk, "rate": steps / mk}), flush=True)
     one1 = out["worlds"].get("1")
     if one1:
         for k, v in out["worlds"].items():
             v["speedup_vs_1"] = one1["makespan_s"] / v["makespan_s"]
             v["makespan_frac_of_1"] = v["makespan_s"] / one1["makespan_s"]
+    # the heaviest ray alone (its attempts from the 1-rank run), and the
+    # heaviest few as one set (C5: its own chunked launches)
+    kw_1 = dict(kw)
+    if a.config == "C5":
+        kw_1["chunk"] = a.chunk or bench.c5_rows_per_launch(a.fields == "fp32", 1, nt)
+    full = run_sharded(eng, y0, nt, rank=0, world=1, gather=False, **kw_1)
+    work = (full.res.nacc + full.res.nrej)
+    ikw = dict(ttotal=(nt - 1) * 7200.0)
+    if a.config == "C5":
+        ikw.update(order_policy="cell", chunk=kw_1["chunk"], team=team, first_chunk=lead)
+    for n in ([1, 8, 64] if a.config == "C5" else [1]):
+        top = torch.topk(work, n).indices
+        rays = y0[:, full.idx[top]].contiguous()
+        dt, r1 = timed(lambda: eng.integrate(rays, nt, 7200.0, **ikw))
+        att = (r1.nacc + r1.nrej)
+        key = "heaviest_ray" if n == 1 else f"heaviest_{n}"
+        out[key] = {"slot": int(full.idx[top[0]].item()), "attempts": int(att.max().item()), "s": dt,
+                    "us_per_attempt": 1e6 * dt / max(int(att.max().item()), 1)}
+        print(json.dumps({key: out[key]}), flush=True)
     if a.config == "C5":
         js = json.dumps(out)
         print(js)
         if a.out:
             open(a.out, "w").write(js + "\n")
         return
-    # the heaviest ray alone (its attempts from the 1-rank run)
-    full = run_sharded(eng, y0, nt, rank=0, world=1, gather=False)
-    work = (full.res.nacc + full.res.nrej)
-    j = int(torch.argmax(work).item())
-    one = y0[:, full.idx[j]:full.idx[j] + 1].contiguous()
-    dt, r1 = timed(lambda: eng.integrate(one, nt, 7200.0, ttotal=(nt - 1) * 7200.0))
-    att = int((r1.nacc + r1.nrej).sum().item())
-    out["heaviest_ray"] = {"slot": int(full.idx[j].item()), "attempts": att, "s": dt,
-                           "us_per_attempt": 1e6 * dt / max(att, 1)}
     w = work[work > 0].double()
     q = torch.tensor([0.5, 0.9, 0.99, 0.999, 0.9999], dtype=torch.float64, device=w.device)
     out["attempts_per_live_ray"] = {"mean": float(w.mean()), "max": int(w.max()),
