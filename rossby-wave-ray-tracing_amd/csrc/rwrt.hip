@@ -989,6 +989,103 @@ __device__ __forceinline__ void lookup_end(const CachedVaryingBG64& B,
   B.end(p, g);
 }
 
+// fp64 levels at 32 rays per wave (rwrt_ctx_set_tv_lanes 32), lane pairs
+// (round 5): lanes L and L + 32 hold the same ray (the same state, the same
+// operations -- run_rays<.., kPair>), and each caches ONE bracketing level in
+// its own slice column: lane L the lower level, lane L + 32 the upper, at the
+// LDS addresses the single-lane layout used (the upper level in lane L + 32's
+// column).  A refill is then 24 LDS-DMA instructions for the wave with both
+// halves active instead of 48 with one half, and each lane blends 11 fields
+// instead of 22; v_permlane32_swap hands every lane both levels' blends
+// (lanes 0-31's in one register, lanes 32-63's in the other), so the time
+// interpolation g_A (1 - w) + g_B w is the same operation on the same values
+// as VaryingBG<double>::interp11 -- bit for bit.
+#ifndef RWRT_TV_PAIR
+#define RWRT_TV_PAIR 1
+#endif
+struct PairVaryingBG64 {
+  static constexpr bool kTimeVarying = true;
+  VaryingBG<double> V;
+  char* wave_base;
+  unsigned lane16;   // this lane's slice column (lane * 16)
+  bool upper;        // lanes 32-63: the upper bracketing level
+  mutable unsigned key_x, key_y;
+  mutable int key_j;
+
+  struct Pending {
+    double w[4];
+    double wt;
+  };
+  __device__ __forceinline__ Pending begin(double lon, double lat, double t) const {
+    Pending p;
+    unsigned o[4], kx, ky;
+    int jl;
+    V.cell(lon, lat, o, p.w, kx, ky);
+    const double* A = V.level(t, p.wt, jl);
+    if (kx != key_x || ky != key_y || jl != key_j) {   // miss (both lanes of the pair): refill by LDS-DMA
+      const double* L = (upper && V.nlev > 1) ? A + V.lev_stride : A;
+      char* const base = lds_slice_base(wave_base);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int q = 0; q < 6; ++q)
+          __builtin_amdgcn_global_load_lds((global_void_ptr)(L + o[j] + 2 * q),
+                                           (lds_void_ptr)(base + (j * 6 + q) * 1024), 16, 0, 0);
+      key_x = kx;
+      key_y = ky;
+      key_j = jl;
+    }
+    return p;
+  }
+  // both lanes' values of x: (lanes 0-31's, lanes 32-63's) on every lane
+  __device__ __forceinline__ static void both(double x, double& a, double& b) {
+    const unsigned lo = (unsigned)__double2loint(x), hi = (unsigned)__double2hiint(x);
+    const auto l = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto h = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    a = __hiloint2double((int)h[0], (int)l[0]);
+    b = __hiloint2double((int)h[1], (int)l[1]);
+  }
+  __device__ __forceinline__ void end(const Pending& p, double g[11]) const {
+    lds_dma_wait();
+    double2 v[4][6];
+#pragma unroll
+    for (int q = 0; q < 6; ++q)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        v[j][q] = *reinterpret_cast<const double2*>(wave_base + (j * 6 + q) * 1024 + lane16);
+    __builtin_amdgcn_sched_barrier(0);
+    double go[11];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      go[2 * q] = VaryingBG<double>::bl(p.w, v[0][q].x, v[1][q].x, v[2][q].x, v[3][q].x);
+      if (2 * q + 1 < 11) go[2 * q + 1] = VaryingBG<double>::bl(p.w, v[0][q].y, v[1][q].y, v[2][q].y, v[3][q].y);
+    }
+#pragma unroll
+    for (int i = 0; i < 11; ++i) {
+      double ga, gb;
+      both(go[i], ga, gb);
+      g[i] = ga * (1.0 - p.wt) + gb * p.wt;
+    }
+  }
+  __device__ __forceinline__ void interp4(double lon, double lat, double t, double& fu, double& fv,
+                                          double& fqx, double& fqy) const {
+    V.interp4(lon, lat, t, fu, fv, fqx, fqy);
+  }
+  __device__ static PairVaryingBG64 make(const VaryingBG<double>& B, char* lds) {
+    const unsigned wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    return PairVaryingBG64{B, lds + wave * kCacheBytesPerWave, (threadIdx.x & 63u) * 16u,
+                           (threadIdx.x & 63u) >= 32u, ~0u, ~0u, -1};
+  }
+};
+__device__ __forceinline__ PairVaryingBG64::Pending lookup_begin(const PairVaryingBG64& B, double lon, double lat,
+                                                                 double t) {
+  return B.begin(lon, lat, t);
+}
+__device__ __forceinline__ void lookup_end(const PairVaryingBG64& B, const PairVaryingBG64::Pending& p,
+                                           double g[11]) {
+  B.end(p, g);
+}
+
 // Latency mode of the time-varying ray loops (rk45_run_kernel's first
 // heavy_blocks blocks, run_rays<.., kReplica>): ONE ray per wavefront,
 // replicated on all 64 lanes (the same state and the same operations on every
@@ -2823,11 +2920,12 @@ struct TvBlock<VaryingBG<T>> {
 // work queue (hw = -1), or -- kReplica, the time-varying latency mode -- every
 // lane of the wave runs the ray at order position hw, replicated, through a
 // BlockVaryingBG, and lane 0 stores its rows and state.
-template <class BG, class LBG, bool kTrace, bool kReplica>
+template <class BG, class LBG, bool kTrace, bool kReplica, bool kPair = false>
 __device__ __forceinline__ void run_rays(const RunArgs<BG>& a, const LBG& lbg, char* smem, int64_t hw) {
   using RayProblem = RayProblemT<LBG>;
   const RayProblem P{lbg};
-  const bool writer = !kReplica || (threadIdx.x & 63u) == 0;   // (a latency wave's lane 0 stores)
+  // (a latency wave's lane 0 stores; lane pairs: the lower lane)
+  const bool writer = kReplica ? (threadIdx.x & 63u) == 0 : kPair ? (threadIdx.x & 63u) < 32u : true;
   const int64_t nrows = a.it_end - a.it_begin;
   Lane<RayProblem, KStore> L;
   L.K.p = reinterpret_cast<double*>(smem) + threadIdx.x;
@@ -2848,6 +2946,10 @@ __device__ __forceinline__ void run_rays(const RunArgs<BG>& a, const LBG& lbg, c
         if (hw < 0) break;
         w = hw;
         hw = -1;
+      } else if (kPair) {   // lane pairs: the lower lane pulls, the upper one takes the same ray
+        int64_t w0 = 0;
+        if ((threadIdx.x & 63u) < 32u) w0 = a.n_heavy + atomicAdd(&a.queue[1], 1);
+        w = __shfl(w0, (int)(threadIdx.x & 31u));
       } else {
         w = a.n_heavy + atomicAdd(&a.queue[1], 1);
       }
@@ -2966,7 +3068,7 @@ __device__ __forceinline__ void run_rays(const RunArgs<BG>& a, const LBG& lbg, c
 #endif
       ray = -1;
     }
-    if (kReplica && it == a.it_end) ray = -1;   // (the other lanes of a latency wave)
+    if ((kReplica || kPair) && it == a.it_end) ray = -1;   // (the other lanes of a latency wave or pair)
   }
 }
 
@@ -3002,7 +3104,14 @@ rk45_run_kernel(RunArgs<BG> a) {
     }
   }
   if constexpr (std::is_same<BG, VaryingBG<double>>::value) {
-    if (a.B.half && (threadIdx.x & 63u) >= 32u) return;   // half density: lanes 32-63's LDS slots hold the upper level
+    if (a.B.half) {   // (kernel-uniform) 32 rays per wave
+#if RWRT_TV_PAIR
+      run_rays<BG, PairVaryingBG64, false, false, true>(a, PairVaryingBG64::make(a.B, smem + kKBytes), smem, -1);
+      return;
+#else
+      if ((threadIdx.x & 63u) >= 32u) return;   // lanes 32-63's LDS slots hold the upper level
+#endif
+    }
   }
   run_rays<BG, typename LaneBG<BG>::type, kTrace, false>(a, LaneBG<BG>::make(a.B, smem + kKBytes), smem, -1);
 }
