@@ -25,6 +25,9 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "rossby-wave-ray-tracing_amd")]
+# (each world size allocates row buffers of another size: without expandable
+# segments the allocator's cached blocks fragment the 288 GB)
+os.environ.setdefault("PYTORCH_ALLOC_CONF", "expandable_segments:True")
 import torch  # noqa: E402
 import bench  # noqa: E402
 from engine import RayEngine  # noqa: E402
