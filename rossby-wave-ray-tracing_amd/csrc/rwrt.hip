@@ -2195,6 +2195,7 @@ struct Lane {
   // the caller sets aux[NAUX-1] = NaN whenever y changes otherwise)
   double aux[P::NAUX > 0 ? P::NAUX : 1];
   double t, habs, hs;
+  double tk6 = 0.0;   // the time of the last accepted step's K6 evaluation (t_old + h), aux's time
   bool in_step, rejected;
 
   // Returns kStep (attempt made, interval not finished), kReached (t == t_bound)
@@ -2241,6 +2242,7 @@ struct Lane {
     const double tnew = (tn != tn) ? tb : tn;              // rkf45.py:503
     habs = acc ? ha * fac : habs;
     hs = acc ? hs : ha * np_max(kMinFactor, sp);
+    tk6 = acc ? t + h : tk6;                                // (dp54_attempt's last stage time)
     t = acc ? tnew : t;
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
@@ -2995,9 +2997,15 @@ __device__ __forceinline__ void run_rays(const RunArgs<BG>& a, const LBG& lbg, c
     // inputs, same operations), so they are reused unless that evaluation was
     // masked (aux NaN) or y has changed since.
     double* y = L.y;
-    // (a time-varying flow recomputes at t_bound: K6 was evaluated at t + h,
-    // which can differ from t_bound in the last bit)
-    const bool have = !BG::kTimeVarying && !isnan(L.aux[2]);
+    // (a time-varying flow: K6 was evaluated at t + h, which can differ from
+    // t_bound in the last bit -- its values are reused only when it does not:
+    // t + (t_bound - t) == t_bound whenever t_bound / 2 <= t, i.e. at every
+    // row end but the first few; otherwise ugvg_at recomputes at t_bound,
+    // an HBM round trip per row end at 0.25 degrees)
+#ifndef RWRT_TV_REUSE_K6
+#define RWRT_TV_REUSE_K6 1
+#endif
+    const bool have = (!BG::kTimeVarying || (RWRT_TV_REUSE_K6 && L.tk6 == tb)) && !isnan(L.aux[2]);
     double ug, vg, cos_c = kNaN;
     bool masked = fabs(y[1]) >= kHalfPi;
     if (!masked) {
