@@ -25,9 +25,6 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "rossby-wave-ray-tracing_amd")]
-# (each world size allocates row buffers of another size: without expandable
-# segments the allocator's cached blocks fragment the 288 GB)
-os.environ.setdefault("PYTORCH_ALLOC_CONF", "expandable_segments:True")
 import torch  # noqa: E402
 import bench  # noqa: E402
 from engine import RayEngine  # noqa: E402
@@ -119,11 +116,14 @@ def main():
             kw_w["costs"] = probe_costs(eng, st0, p, tb, 6, 0, w)
             del st0
         for r in range(w):
+            torch.cuda.empty_cache()   # (row buffers of another size cached by the allocator)
             dt, res = timed(lambda: run_sharded(eng, y0, nt, rank=r, world=w, gather=False,
                                                        team=team, lead=lead, **kw_w), reps=a.reps)
             ev = []
+            del res
+            torch.cuda.empty_cache()
             eng.keep_launch_work = True
-            run_sharded(eng, y0, nt, rank=r, world=w, gather=False, team=team, lead=lead, events=ev, **kw_w)
+            res = run_sharded(eng, y0, nt, rank=r, world=w, gather=False, team=team, lead=lead, events=ev, **kw_w)
             torch.cuda.synchronize()
             eng.keep_launch_work = False
             # the last launch's heaviest rays: attempts there, and whether the
