@@ -735,10 +735,11 @@ def c5_rows_per_launch(fp32, world, nt):
     the horizon when a set is split (N = 2 / 4 / 8: 1.67-1.72 / 0.99 / 0.78 s
     against 1.90 / 1.52 / 1.34 s at 96-row or 48-row launches: a shard's
     heaviest rays then run their chains without a barrier;
-    profiles/r5/sched/c5_half_*.json)."""
-    if fp32:
-        return 240
-    return 144 if world <= 1 else nt - 1
+    profiles/r5/sched/c5_half_*.json); fp32 levels likewise when split (8
+    shards 1.55 s at 240-row launches, profiles/r5/final4/c5_fp32_rehearsal.json)."""
+    if world > 1:
+        return nt - 1
+    return 240 if fp32 else 144
 
 
 def main_c5(args, dist, group, rank, world, dev, share=1):
