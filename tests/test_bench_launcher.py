@@ -111,8 +111,9 @@ def test_schedule_defaults():
     assert (a.first_chunk, a.probe, a.team) == ("24,96", 6, "auto")
     a = bench.schedule_defaults(ns(scaling="strong"), 1)
     assert (a.first_chunk, a.probe, a.team) == ("24,160", 4, "64,64,64")
+    # C5: no latency mode by default (its launch-ending rays are not predictable)
     a = bench.schedule_defaults(ns(config="C5"), 1)
-    assert (a.first_chunk, a.probe, a.team) == ("24,96", 6, "auto")
+    assert (a.first_chunk, a.probe, a.team) == ("24,96", 6, "0")
     a = bench.schedule_defaults(ns(probe=6, team="0", first_chunk="24"), 1)
     assert (a.first_chunk, a.probe, a.team) == ("24", 6, "0")
 
