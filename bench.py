@@ -731,18 +731,21 @@ def c5_parity_sample(eng, rows_all, fields, dev):
 
 
 def c5_rows_per_launch(fp32, world, nt):
-    """C5's rows per launch of the long launches (before the memory cap):
-    fp32 levels 240 (profiles/r1/c5/chunk_sweep.txt); fp64 levels, 32 rays per
-    wave with both levels cached (RayEngine.tv_lanes), 144 on one GPU (72 /
-    96 / 144 / 192 rows: 2.72 / 2.70 / 2.69 / 2.81 s) and the whole rest of
-    the horizon when a set is split (N = 2 / 4 / 8: 1.67-1.72 / 0.99 / 0.78 s
-    against 1.90 / 1.52 / 1.34 s at 96-row or 48-row launches: a shard's
-    heaviest rays then run their chains without a barrier;
-    profiles/r5/sched/c5_half_*.json); fp32 levels likewise when split (8
-    shards 1.55 s at 240-row launches, profiles/r5/final4/c5_fp32_rehearsal.json)."""
+    """C5's rows per launch of the long launches (before the memory cap).
+    One GPU (round 5 final build, lane pairs and row-end reuse; one box):
+    fp64 levels 96 rows (48 / 72 / 96 / 120 / 144: 1.54 / 1.59 / 1.61 / 1.59 /
+    1.47e9 ray-steps/s -- each launch re-sorts the queue by cost class and
+    grid cell, and the fp64 lookups gain from that locality), fp32 levels 360
+    (240 / 360 / 540 / 1080: 1.56 / 1.59 / 1.46 / 1.49e9;
+    profiles/r5/final4/c5_chunk_sweep.txt).  A split set runs the whole rest
+    of the horizon in one launch (fp64, N = 2 / 4 / 8: 1.67-1.72 / 0.99 /
+    0.78 s against 1.90 / 1.52 / 1.34 s at 96-row or 48-row launches: a
+    shard's heaviest rays then run their chains without a barrier,
+    profiles/r5/sched/c5_half_*.json; fp32 levels 8 shards 0.85 s against
+    1.55 s at 240-row launches, profiles/r5/final4/c5_fp32_rehearsal*.json)."""
     if world > 1:
         return nt - 1
-    return 240 if fp32 else 144
+    return 360 if fp32 else 96
 
 
 def main_c5(args, dist, group, rank, world, dev, share=1):
