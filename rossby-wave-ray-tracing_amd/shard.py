@@ -280,8 +280,8 @@ class ShardedRun:
         self.idx = idx                  # this rank's rays (device index tensor)
         self.res = res                  # engine.RunResult of the shard (None if failed)
         self.steps_local = steps_local  # accepted steps of this rank's rays
-        self.endpoints = endpoints      # rank 0: last row [nray, 8] of every ray
-        self.counts = counts            # rank 0: [nray, 2] accepted / rejected
+        self.endpoints = endpoints      # rank 0: last row [nray, 8] of every ray (an emulated rank: its own, idx order)
+        self.counts = counts            # rank 0: [nray, 2] accepted / rejected (likewise)
         self.failed = failed
 
 
@@ -384,6 +384,6 @@ def run_sharded(eng, y0, nt, tstep=7200.0, group=None, rank=None, world=None, pr
         if group is not None and world > 1:
             ends = gather_rows(end_row, idx.cpu().numpy(), nray, group=group)
             cnts = gather_rows(local["count"], idx.cpu().numpy(), nray, group=group)
-        elif world == 1:
+        else:   # (one rank, or one emulated rank of a larger job: its own rays, in idx order)
             ends, cnts = end_row, local["count"]
     return ShardedRun(idx, res, steps_local, ends, cnts)

@@ -152,6 +152,48 @@ def test_c4_cost_sharded_world2_equals_single_gpu(shard_probe):
     assert same(ends, hist[:, -1])
 
 
+@pytest.mark.parametrize("world", [8])
+def test_c4_full_set_split_union_equals_single_gpu(world):
+    """The WHOLE C3 set (2.40 M slots, 12 days) split ``world`` ways as
+    bench.py --gpus 8 splits it -- each rank probing every ``world``-th ray,
+    the costs all-gathered (here: every share probed on this GPU,
+    shard.probe_costs), each rank re-probing and integrating its shard --
+    each emulated rank run alone on this GPU: the union of the ranks' last
+    rows and step counters equals the 1-GPU run's bit for bit, and the split
+    is disjoint, complete and balanced in live rays."""
+    import torch
+    from bench import c3_initial_state, make_bs
+    from engine import RayEngine, t_eval_of
+    from shard import probe_costs, run_sharded
+    bs, _ = make_bs("zonal")
+    eng = RayEngine.from_bs(bs)
+    y0 = torch.as_tensor(c3_initial_state(bs), device=eng.device)
+    nt = C3_DAYS * 12 + 1
+    one = run_sharded(eng, y0, nt, rank=0, world=1, lead=[24, 96])
+    ends1, cnt1 = one.endpoints.cpu().numpy(), one.counts.cpu().numpy()
+    p = eng.params(nt, 7200.0)
+    st0 = eng.init(y0, p)
+    tb = torch.as_tensor(t_eval_of(nt, 7200.0), dtype=torch.float64, device=eng.device)
+    costs = probe_costs(eng, st0, p, tb, 6, 0, world)
+    del st0
+    nray = y0.shape[1]
+    ends = np.full((nray, 8), -1.0)
+    cnts = np.full((nray, 2), -1, dtype=np.int64)
+    seen = np.zeros(nray, dtype=np.int64)
+    live = []
+    for r in range(world):
+        rr = run_sharded(eng, y0, nt, rank=r, world=world, lead=[24, 96], costs=costs)
+        idx = rr.idx.cpu().numpy()
+        seen[idx] += 1
+        ends[idx] = rr.endpoints.cpu().numpy()
+        cnts[idx] = rr.counts.cpu().numpy()
+        live.append(int((~torch.isnan(y0[:, rr.idx].sum(0))).sum().item()))
+    assert (seen == 1).all()                                   # disjoint and complete
+    assert max(live) - min(live) <= 2                          # balanced in live rays
+    assert np.array_equal(cnts, cnt1)
+    assert same(ends, ends1), f"{ndiff(ends, ends1)} values differ"
+
+
 @pytest.mark.refhost
 # ---------------------------------------------------------------- C5
 @pytest.mark.parametrize("fp32", [False, True])
