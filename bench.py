@@ -587,8 +587,11 @@ def main():
                    f"accepted-step counts are gathered to rank 0 (RCCL gather)")
         else:
             par = (f"one ray set over {world} GPU(s): cost-balanced split by a "
-                   f"{args.probe}-row probe, RCCL broadcast of the basic state and "
-                   f"gather of endpoints + step counters inside the timed step")
+                   f"{args.probe}-row probe" +
+                   (" (each rank probes 1/N of the rays, the costs all-gathered)" if world > 1 and args.shard_probe
+                    else "") +
+                   ", RCCL broadcast of the basic state and gather of endpoints + step counters inside the "
+                   "timed step")
         ends0 = gathered.get("rank0") if weak else r.endpoints[live_idx.to(r.endpoints.device)]
         result = {
             "metric": METRIC, "value": value, "unit": "ray-steps/s", "n_gpus": world,
