@@ -156,8 +156,10 @@ def main():
     # the heaviest ray alone (its attempts from the 1-rank run), and the
     # heaviest few as one set (C5: its own chunked launches)
     kw_1 = dict(kw)
-    if a.config == "C5":
-        kw_1["chunk"] = a.chunk or bench.c5_rows_per_launch(a.fields == "fp32", 1, nt)
+    if a.config == "C5":   # (capped by the row buffer's memory, as bench.py main_c5 caps it)
+        torch.cuda.empty_cache()
+        cap = max(1, int(0.8 * torch.cuda.mem_get_info()[0]) // ((int(y0.shape[1]) + 2) * 64))
+        kw_1["chunk"] = min(a.chunk or bench.c5_rows_per_launch(a.fields == "fp32", 1, nt), cap)
     full = run_sharded(eng, y0, nt, rank=0, world=1, gather=False, **kw_1)
     work = (full.res.nacc + full.res.nrej)
     ikw = dict(ttotal=(nt - 1) * 7200.0)
