@@ -745,9 +745,13 @@ def c5_rows_per_launch(fp32, world, nt):
     0.78 s against 1.90 / 1.52 / 1.34 s at 96-row or 48-row launches: a
     shard's heaviest rays then run their chains without a barrier,
     profiles/r5/sched/c5_half_*.json; fp32 levels 8 shards 0.85 s against
-    1.55 s at 240-row launches, profiles/r5/final4/c5_fp32_rehearsal*.json)."""
+    1.55 s at 240-row launches, profiles/r5/final4/c5_fp32_rehearsal*.json)
+    -- except fp64 levels split 2 ways, whose shards are still throughput-bound:
+    96 rows, 1.47 s against 1.54 s at 144 and 1.66 s in one launch (4 / 8
+    shards at 96 rows: 1.27 / 1.09 s against 0.96 / 0.71 in one launch;
+    profiles/r5/final5/c5_split_chunks.txt)."""
     if world > 1:
-        return nt - 1
+        return 96 if (world == 2 and not fp32) else nt - 1
     return 360 if fp32 else 96
 
 
