@@ -102,10 +102,11 @@ rwrt_status rwrt_ctx_set_latency_density(rwrt_ctx* ctx, int32_t rays_per_wave);
 /* Rays per wavefront of this context's fp64 time-varying ray loops
  * (rwrt_rk45_run_tv*, levels with fp32 == 0): 64 (default; the lower
  * bracketing level cached per lane in LDS, the upper one gathered) or 32
- * (each lane caches both levels, using the LDS of a second lane: no HBM
- * gathers while a ray stays in its cell and level pair -- shorter attempts
- * for the few long rays that end a launch, half the lanes).  Schedule only:
- * results do not depend on it (ABI 3). */
+ * (lane pairs: lanes L and L + 32 run the same ray, each caching and blending
+ * one bracketing level, exchanged by v_permlane32_swap -- no HBM gathers
+ * while a ray stays in its cell and level pair, half the LDS-DMA per refill;
+ * RayEngine's default, C5 fp64 1.21 -> 1.61e9 with the other round-5 changes).
+ * Schedule only: results do not depend on it (ABI 3). */
 rwrt_status rwrt_ctx_set_tv_lanes(rwrt_ctx* ctx, int32_t lanes);
 /* Diagnostic ray trace of the context's rwrt_rk45_run calls (NULL / 0: off):
  * for queue positions w < capacity of the order, the ray's lane records
