@@ -278,29 +278,15 @@ struct SinCosPre {
 // The two evaluations read the table points of x and x (below 0.855469) or
 // of a = t + pi/2 tail and t (above), and a is within an ulp of t: the two
 // points are one unless t lies within an ulp of a 1/128 rounding midpoint.
-// NM_SINCOS_SHARED_ENTRY=1 reads one entry and the second only on that rare
-// branch (half the lane-random table reads, which are the kernels' LDS bank
-// conflicts: 0.187 -> 0.148 of LDS-active cycles), made wave-uniform -- as a
-// divergent branch the compiler mis-scheduled it in attempt_kernel (a stage
-// value read as 0.0).  Measured 0.955x on C3 (the ballot's SGPRs add spill
-// moves to the run kernel, profiles/r5/sched/sincos_entry.txt): off.
-#ifndef NM_SINCOS_SHARED_ENTRY
-#define NM_SINCOS_SHARED_ENTRY 0
-#endif
+// (Reading one entry, and the second only where the two differ, halves the
+// lane-random table reads -- the kernels' LDS bank conflicts, 0.187 -> 0.148
+// of LDS-active cycles -- but measured 0.955x on C3: the wave-uniform branch's
+// SGPRs add spill moves to the run kernel, profiles/r5/sched/sincos_entry.txt.)
 NM_FN SinCosPre nm_sincos_tab(double x) {
   const bool far = g_hi(x) >= 0x3FEB6000u;
   const double t = nm_d(kG_HP0) - nm_abs(x);
   const double a = t + nm_d(kG_HP1);
-#if NM_SINCOS_SHARED_ENTRY
-  const unsigned ks = g_index(far ? a : x), kc = g_index(far ? t : x);
-  SinCosPre P;
-  P.Ts = g_tab(ks);
-  P.Tc = P.Ts;
-  if (NM_RARE_ANY(kc != ks)) P.Tc = g_tab(kc);   // (g_tab(kc) == P.Ts where kc == ks)
-  return P;
-#else
   return SinCosPre{g_tab(g_index(far ? a : x)), g_tab(g_index(far ? t : x))};
-#endif
 }
 NM_FN void nm_sincos_fin(double x, const SinCosPre& P, double& sn, double& cs) {
   const unsigned k = g_hi(x);

@@ -452,9 +452,6 @@ constexpr int kCacheAhead = 1;
 // loads only (chunks 0-3, vmcnt(8)); the wait for all 24 sits before the
 // read of chunk 4 -- a read-ahead of 4 or more would read chunk 4 early
 static_assert(kCacheAhead >= 0 && kCacheAhead < 4, "end() prologue waits for chunks 0-3 only");
-#ifndef RWRT_KAP_IN_LOOKUP   // the wavenumber terms under the cell cache's first reads: +0.3 % (r4e)
-#define RWRT_KAP_IN_LOOKUP 1
-#endif
 
 // The cache image of the static state: the records of 64 consecutive grid
 // points stored chunk-major, so that a corner's six 16-B chunks lie 1 KiB
@@ -887,9 +884,6 @@ struct CachedVaryingBG64 {
   unsigned lane16;
   mutable unsigned key_x, key_y;
   mutable int key_j;
-#ifdef RWRT_TV_MISS_DIAG
-  mutable unsigned misses = 0;   // (diagnostic build: refills made by this lane)
-#endif
 
   struct Pending {
     double w[4];
@@ -908,9 +902,6 @@ struct CachedVaryingBG64 {
     const double* A = V.level(t, p.wt, jl);
     p.B = A + (V.nlev > 1 ? V.lev_stride : 0);
     if (kx != key_x || ky != key_y || jl != key_j) {   // miss: refill by LDS-DMA
-#ifdef RWRT_TV_MISS_DIAG
-      ++misses;
-#endif
       char* const base = lds_slice_base(wave_base);
 #pragma unroll
       for (int j = 0; j < 4; ++j)
@@ -1000,9 +991,6 @@ __device__ __forceinline__ void lookup_end(const CachedVaryingBG64& B,
 // (lanes 0-31's in one register, lanes 32-63's in the other), so the time
 // interpolation g_A (1 - w) + g_B w is the same operation on the same values
 // as VaryingBG<double>::interp11 -- bit for bit.
-#ifndef RWRT_TV_PAIR
-#define RWRT_TV_PAIR 1
-#endif
 struct PairVaryingBG64 {
   static constexpr bool kTimeVarying = true;
   VaryingBG<double> V;
@@ -1060,6 +1048,7 @@ struct PairVaryingBG64 {
       go[2 * q] = VaryingBG<double>::bl(p.w, v[0][q].x, v[1][q].x, v[2][q].x, v[3][q].x);
       if (2 * q + 1 < 11) go[2 * q + 1] = VaryingBG<double>::bl(p.w, v[0][q].y, v[1][q].y, v[2][q].y, v[3][q].y);
     }
+    MARK("p_blend");
 #pragma unroll
     for (int i = 0; i < 11; ++i) {
       double ga, gb;
@@ -1238,22 +1227,6 @@ struct LaneBG<VaryingBGA32> {
     return c;
   }
 };
-// RWRT_TV64_TWO_WAVES: the fp64 time-varying ray loop at two waves per SIMD
-// without the lower level's LDS cache (two blocks' caches do not fit a CU's
-// LDS): a second wave to hide the level gathers' latency (A/B build)
-#ifndef RWRT_TV64_TWO_WAVES
-#define RWRT_TV64_TWO_WAVES 0
-#endif
-template <class BG>
-struct RunWaves {
-  static constexpr int kPerSimd = 1;
-};
-#if RWRT_TV64_TWO_WAVES
-template <>
-struct RunWaves<VaryingBG<double>> {
-  static constexpr int kPerSimd = 2;
-};
-#else
 template <>
 struct LaneBG<VaryingBG<double>> {
   using type = CachedVaryingBG64;
@@ -1263,7 +1236,6 @@ struct LaneBG<VaryingBG<double>> {
     return CachedVaryingBG64{B, lds + wave * kCacheBytesPerWave, (threadIdx.x & 63u) * 16u, ~0u, ~0u, -1};
   }
 };
-#endif
 
 }  // namespace rwrt
 
@@ -1327,10 +1299,6 @@ __device__ __forceinline__ double add_rd(double a, double b) {
 // array, where the flat table put the pairs of the 64 lanes' lane-random
 // reads in 8 slots -- tan's, log's and exp's (head, tail) pairs, the knots'
 // (A, N) pairs.  Same values, so the same results.
-#ifndef RWRT_NM_INTERLEAVED
-#define RWRT_NM_INTERLEAVED 1
-#endif
-#if RWRT_NM_INTERLEAVED
 __shared__ __attribute__((aligned(16))) double2 nm_lds_sc_s[110];    // kG_SINCOSTAB[4j], [4j + 1]
 __shared__ __attribute__((aligned(16))) double2 nm_lds_sc_c[110];    // kG_SINCOSTAB[4j + 2], [4j + 3]
 __shared__ __attribute__((aligned(16))) double2 nm_lds_tan[16];      // kT_TAN_HI[j], kT_TAN_LO[j]
@@ -1362,17 +1330,6 @@ __shared__ __attribute__((aligned(8))) uint2 nm_lds_knot[64];        // kRCP14_K
     n = nm_k_.y;                             \
   } while (0)
 #define NM_LD(t, i) NM_LD_unused_##t
-#else   // (round 4's flat tables: A/B)
-__shared__ unsigned long long nm_lds_kG_SINCOSTAB[440];
-__shared__ unsigned long long nm_lds_kT_TAN_HI[16];
-__shared__ unsigned long long nm_lds_kT_TAN_LO[16];
-__shared__ unsigned long long nm_lds_kP_LOG_HI[32];
-__shared__ unsigned long long nm_lds_kP_LOG_LO[32];
-__shared__ unsigned long long nm_lds_kP_EXP_HI[16];
-__shared__ unsigned long long nm_lds_kP_EXP_LO[16];
-__shared__ unsigned nm_lds_kRCP14_KNOT[128];
-#define NM_LD(t, i) nm_lds_##t[i]
-#endif
 // (The polynomial constants stay s_mov_b32 pairs: as scalar loads they share
 // lgkmcnt with the LDS reads, 0.99x; from LDS the round trip lands on the
 // polynomial chains, 0.91x -- profiles/r2/ab/const_lds.txt.)
@@ -1387,26 +1344,6 @@ enum { NM_SINCOS = 1, NM_TAN = 2, NM_POW = 4, NM_ALL = 7 };
 template <int MASK>
 __device__ __forceinline__ void nm_stage() {
   const int t = threadIdx.x, nt = blockDim.x;
-#if !RWRT_NM_INTERLEAVED
-  if (MASK & NM_SINCOS)
-    for (int i = t; i < 440; i += nt) nm_lds_kG_SINCOSTAB[i] = np_math::kG_SINCOSTAB[i];
-  if (MASK & NM_TAN)
-    for (int i = t; i < 16; i += nt) {
-      nm_lds_kT_TAN_HI[i] = np_math::kT_TAN_HI[i];
-      nm_lds_kT_TAN_LO[i] = np_math::kT_TAN_LO[i];
-    }
-  if (MASK & NM_POW)
-    for (int i = t; i < 32; i += nt) {
-      nm_lds_kP_LOG_HI[i] = np_math::kP_LOG_HI[i];
-      nm_lds_kP_LOG_LO[i] = np_math::kP_LOG_LO[i];
-      if (i < 16) {
-        nm_lds_kP_EXP_HI[i] = np_math::kP_EXP_HI[i];
-        nm_lds_kP_EXP_LO[i] = np_math::kP_EXP_LO[i];
-      }
-    }
-  if (MASK & (NM_TAN | NM_POW))
-    for (int i = t; i < 128; i += nt) nm_lds_kRCP14_KNOT[i] = np_math::kRCP14_KNOT[i];
-#else
   auto d = [](unsigned long long u) { return __builtin_bit_cast(double, u); };
   if (MASK & NM_SINCOS)
     for (int i = t; i < 110; i += nt) {
@@ -1422,7 +1359,6 @@ __device__ __forceinline__ void nm_stage() {
     }
   if (MASK & (NM_TAN | NM_POW))
     for (int i = t; i < 64; i += nt) nm_lds_knot[i] = make_uint2(np_math::kRCP14_KNOT[2 * i], np_math::kRCP14_KNOT[2 * i + 1]);
-#endif
   __syncthreads();
 }
 
@@ -1683,30 +1619,28 @@ __device__ __forceinline__ void ray_rhs(const BG& B, double t, const double* y, 
   double g[11];
   // the trigonometry's table reads and tan polynomial beside the lookup's cell
   // arithmetic (one scheduling region: the refill below is a branch)
+  MARK("r_entry");
   const auto trig = np_math::nm_sincostan_begin(lat);
+  MARK("r_trig_begin");
   double s, c;
   DivGuard G;
-#if RWRT_KAP_IN_LOOKUP
   KapTermsR kw;
-#else
-  const KapTermsR kw = kap_terms_r(kx, ky, G);   // (k, l only: beside the trig and the cell arithmetic)
-#endif
   const auto pending = lookup_begin(B, lon, lat, t);   // the lookup's fill overlaps the trig
+  MARK("r_lookup_begin");
   double tn;
   np_math::nm_sincostan_end(lat, trig, s, c, tn);   // == k_sincostan(lat, s, c, tn)
+  MARK("r_trig_end");
   __builtin_amdgcn_sched_barrier(0);
-#if RWRT_KAP_IN_LOOKUP
-  // the wavenumber terms (k, l only) under the cell cache's first reads
-  lookup_end(B, pending, g, [&] { kw = kap_terms_r(kx, ky, G); });
-#else
-  lookup_end(B, pending, g);
-#endif
+  // the wavenumber terms (k, l only) under the cell cache's first reads (+0.3 %, r4e)
+  lookup_end(B, pending, g, [&] { kw = kap_terms_r(kx, ky, G); MARK("r_kap"); });
+  MARK("r_lookup_end");
   const Merc M = merc_factors(lat, c, s);
   double ug, vg;
   if (RARE(!rhs_tail_fast(g, M, s, c, tn, kx, kw, G, amp, dy, ug, vg))) {
     asm volatile("");   // an operand outside qdiv's exact range, or the pole band (rare branch)
     rhs_tail_ieee(g, M, s, c, tn, kx, ky, amp, dy, ug, vg);
   }
+  MARK("r_tail");
   if (aux) {
     aux[0] = ug;
     aux[1] = vg;
@@ -2063,6 +1997,7 @@ __device__ __forceinline__ double dp54_attempt(const P& fun, KS& K, double t, co
         case 5: stage_part<6, 5, NV>(K, f, part); w = kW[6][5]; cn = kCs[6]; break;
         default: error_part<NV>(K, f, part); break;
       }
+      MARK("a_stage_part");
       fun(ts, ys, r, aux);
       if (s < 6) {
         K.put_stage(s, r);
@@ -2070,6 +2005,7 @@ __device__ __forceinline__ double dp54_attempt(const P& fun, KS& K, double t, co
         for (int v = 0; v < NV; ++v) ys[v] = y[v] + (part[v] + r[v] * w) * h;
         ts = t + cn * h;
       }
+      MARK("a_stage_sum");
     }
     double ss = 0.0;
 #pragma unroll
@@ -2228,6 +2164,7 @@ struct Lane {
     double yn[NV], k6[NV];
     double en = dp54_attempt(fun, K, t, y, f, h, rtol, atol, yn, k6, nullptr, 0,
                              P::NAUX > 0 ? aux : nullptr);
+    MARK("a_error_norm");
     if (en != en) en = 0.0;                 // rkf45.py:446
     // SAFETY * error_norm ** (-1/5), shared by the accept (rkf45.py:453-469) and
     // reject (rkf45.py:471-475) factors: one pow per attempt even when the
@@ -2545,20 +2482,6 @@ __device__ __forceinline__ void quad_rhs(const CachedStaticBG& B, const QuadRole
   const double fu = g[F_U], fv = g[F_V];
   // (the mask's factor on a branch, not as selects: 24 v_cndmask per RHS
   // on the common path otherwise)
-#ifndef RWRT_QUAD_MASK_BRANCH
-#define RWRT_QUAD_MASK_BRANCH 1
-#endif
-#if !RWRT_QUAD_MASK_BRANCH   // (round 4: selects)
-  const double fmuy = mk ? (g[F_UY] + tn * fu) * m : g[F_UY] + tn * fu;
-  const double fmvy = mk ? (g[F_VY] + tn * fv) * m : g[F_VY] + tn * fv;
-  const double fmqx = mk ? g[F_QX] * m : g[F_QX];
-  const double fmqy = mk ? (g[F_QY] * cp) * m : g[F_QY] * cp;
-  const double fmqxx = mk ? g[F_QXX] * m : g[F_QXX];
-  const double fmqyx = mk ? (g[F_QXY] * cp) * m : g[F_QXY] * cp;
-  const double fmqxy = mk ? fmqyx * m : fmqyx;
-  const double fmqyy = mk ? (((g[F_QYY] * cp) - (g[F_QY] * M.s)) * cp) * m
-                          : ((g[F_QYY] * cp) - (g[F_QY] * M.s)) * cp;
-#else
   double fmuy = g[F_UY] + tn * fu, fmvy = g[F_VY] + tn * fv;
   double fmqx = g[F_QX], fmqy = g[F_QY] * cp, fmqxx = g[F_QXX], fmqyx = g[F_QXY] * cp;
   double fmqxy = fmqyx, fmqyy = ((g[F_QYY] * cp) - (g[F_QY] * M.s)) * cp;
@@ -2573,7 +2496,6 @@ __device__ __forceinline__ void quad_rhs(const CachedStaticBG& B, const QuadRole
     fmqxy = fmqyx * m;
     fmqyy = fmqyy * m;
   }
-#endif
   const double kap = kw.kap, kap2 = kw.kap2;
   MARK("merc_done");
   // slot 1: the quotients that need no other quotient
@@ -2586,10 +2508,6 @@ __device__ __forceinline__ void quad_rhs(const CachedStaticBG& B, const QuadRole
   }
   const double du = qbcast<0>(q1), dv = qbcast<0>(q2), dux = qbcast<1>(q1), dvx = qbcast<1>(q2);
   const double qu = qbcast<2>(q1), qv = qbcast<2>(q2), qk = qbcast<3>(q1), ql = qbcast<3>(q2);
-#if !RWRT_QUAD_MASK_BRANCH
-  const double fmu = mk ? du * m : du, fmv = mk ? dv * m : dv;
-  const double fmux = mk ? dux * m : dux, fmvx = mk ? dvx * m : dvx;
-#else
   double fmu = du, fmv = dv, fmux = dux, fmvx = dvx;
   if (RARE(mk)) {
     asm volatile("");   // the pole band (rare branch)
@@ -2598,7 +2516,6 @@ __device__ __forceinline__ void quad_rhs(const CachedStaticBG& B, const QuadRole
     fmux = dux * m;
     fmvx = dvx * m;
   }
-#endif
   const double ug = fmu + qu, vg = fmv + qv;                       // cal_ugvg (wn.py:266-294)
   const double dzwn = (-kx) * ((fmux + kap * fmvx) + qk);          // core_diffun (wr.py:53-78)
   const double dmwn = (-kx) * ((fmuy + kap * fmvy) + ql);
@@ -2935,9 +2852,6 @@ __device__ __forceinline__ void run_rays(const RunArgs<BG>& a, const LBG& lbg, c
   int64_t ray = -1, nacc = 0, nrej = 0;
   int32_t it = 0, nanrow = 0, wpos = 0;   // (wpos: the ray's queue position, kTrace only)
   double prev_lon = 0.0, prev_lat = 0.0, cos_prev = 0.0;
-#ifdef RWRT_TV_MISS_DIAG
-  unsigned miss0 = 0;   // (diagnostic build: trace[ray] += the ray's refills, time-varying fp64)
-#endif
   // above frozen_fill_kernel's waves (priority 0) sharing the SIMD: the
   // fill takes the issue cycles the ray loop leaves idle
   __builtin_amdgcn_s_setprio(1);
@@ -2979,9 +2893,6 @@ __device__ __forceinline__ void run_rays(const RunArgs<BG>& a, const LBG& lbg, c
       nrej = a.count[2 * ray + 1];
       nanrow = a.nanrow[ray];
       it = a.it_begin;
-#ifdef RWRT_TV_MISS_DIAG
-      if constexpr (std::is_same<LBG, CachedVaryingBG64>::value) miss0 = P.B.misses;
-#endif
       prev_lon = L.y[0];   // == rlon[it-1], rlat[it-1] (wr.py:844, 877-885)
       prev_lat = L.y[1];
       cos_prev = k_cos(prev_lat);
@@ -3070,10 +2981,6 @@ __device__ __forceinline__ void run_rays(const RunArgs<BG>& a, const LBG& lbg, c
       a.count[2 * ray] = nacc;
       a.count[2 * ray + 1] = nrej;
       a.nanrow[ray] = nanrow;
-#ifdef RWRT_TV_MISS_DIAG
-      if constexpr (std::is_same<LBG, CachedVaryingBG64>::value)
-        if (a.trace && ray < a.trace_cap) a.trace[ray] += (int64_t)(P.B.misses - miss0);
-#endif
       ray = -1;
     }
     if ((kReplica || kPair) && it == a.it_end) ray = -1;   // (the other lanes of a latency wave or pair)
@@ -3081,7 +2988,7 @@ __device__ __forceinline__ void run_rays(const RunArgs<BG>& a, const LBG& lbg, c
 }
 
 template <class BG, bool kTrace = false>
-__global__ void __launch_bounds__(256, RunWaves<BG>::kPerSimd) __attribute__((aligned(RWRT_RUN_ALIGN)))
+__global__ void __launch_bounds__(256, 1) __attribute__((aligned(RWRT_RUN_ALIGN)))
 rk45_run_kernel(RunArgs<BG> a) {
   nm_stage<NM_ALL>();
   // all LDS in one array: the stages (5 x 5 doubles per lane) then the lookup cache
@@ -3112,13 +3019,13 @@ rk45_run_kernel(RunArgs<BG> a) {
     }
   }
   if constexpr (std::is_same<BG, VaryingBG<double>>::value) {
-    if (a.B.half) {   // (kernel-uniform) 32 rays per wave
-#if RWRT_TV_PAIR
+#ifdef RWRT_ANALYZE_PAIR
+    if (true) {   // (analysis build: the lane-pair loop only)
+#else
+    if (a.B.half) {   // (kernel-uniform) 32 rays per wave: lane pairs
+#endif
       run_rays<BG, PairVaryingBG64, false, false, true>(a, PairVaryingBG64::make(a.B, smem + kKBytes), smem, -1);
       return;
-#else
-      if ((threadIdx.x & 63u) >= 32u) return;   // lanes 32-63's LDS slots hold the upper level
-#endif
     }
   }
   run_rays<BG, typename LaneBG<BG>::type, kTrace, false>(a, LaneBG<BG>::make(a.B, smem + kKBytes), smem, -1);
@@ -3888,12 +3795,6 @@ rwrt_status launch_run(rwrt_ctx* ctx, const BG& B, int64_t nray, const rwrt_para
     a.trace = ctx->trace;
     a.trace_cap = ctx->trace ? ctx->trace_cap : 0;
   }
-#ifdef RWRT_TV_MISS_DIAG
-  if constexpr (std::is_same<BG, VaryingBG<double>>::value) {   // (per-ray refill counts, indexed by ray)
-    a.trace = ctx->trace;
-    a.trace_cap = ctx->trace ? ctx->trace_cap : 0;
-  }
-#endif
   if (nray > n_heavy || team_blocks) {
     const int64_t grid = team_blocks + (nray > n_heavy ? blocks : 0);
     if (a.trace && std::is_same<BG, StaticBG>::value) {

@@ -140,16 +140,18 @@ class RayEngine:
         return cls(bs.fields, bs.lon, bs.lat, device)
 
     @classmethod
-    def from_levels(cls, levels):
+    def from_levels(cls, levels, time_varying=None):
         """Engine over a ``levels.Levels`` basic state.  One fp64 level is the
         reference's static state (same kernels, same bits); otherwise the
-        time-varying kernels (``rwrt_rk45_*_tv``) run."""
+        time-varying kernels (``rwrt_rk45_*_tv``) run.  ``time_varying=True``
+        sends one fp64 level through the time-varying kernels too (the test
+        that they reduce to the reference: tests/test_gpu_ref90.py)."""
         self = cls.__new__(cls)
         self.device = levels.device
         self.grid = levels.grid
         self.levels = levels
         self.work = torch.zeros(4, dtype=torch.int32, device=self.device)
-        if levels.nlev == 1 and not levels.fp32:
+        if levels.nlev == 1 and not levels.fp32 and not time_varying:
             self.packed = levels.packed[0]
             self.bg = None
         else:
@@ -406,7 +408,9 @@ class RayEngine:
         cum = torch.cumsum(w, 0)
         best = None
         tv = self.bg is not None   # (time-varying: one ray per latency wave; 32 or 64 run lanes per wave)
-        lanes_cu = (4.0 * self.tv_lanes) if tv else 256.0
+        # (fp64 levels run tv_lanes rays per wave -- rwrt_ctx_set_tv_lanes sets
+        # half only for VaryingBG<double>; fp32-storage levels run 64)
+        lanes_cu = (4.0 * self.tv_lanes) if (tv and self.bg.fp32 == 0) else 256.0
         for q in ((1,) if tv else self.QUAD_DENSITIES):
             cap = min((ncu // 2) * 4 * q, n_live)
             n = torch.arange(0, cap + 1, 4 * q, device=w.device)
@@ -666,7 +670,8 @@ class RayEngine:
             # (a list: one latency-mode size per launch, the last repeated)
             tk = team[min(k, len(team) - 1)] if isinstance(team, list) else team
             if order_policy in ("cost", "priority", "cell", "total") and prev_work is not None:
-                order = (self.cost_cell_order(st, work, head=self.team_capacity_tv() if tk else 0)
+                head = (self.team_capacity_tv() if self.bg is not None else self.team_capacity()) if tk else 0
+                order = (self.cost_cell_order(st, work, head=head)
                          if order_policy == "cell" else self.cost_order(st, work))
             n_heavy, qpw = self.team_size(tk, st, work, order, i1 - i0) if tk else (0, 16)
             self.launch_log.append({"rows": [int(i0), int(i1)], "n_heavy": int(n_heavy), "per_wave": int(qpw)})

@@ -243,8 +243,11 @@ def probe_costs(eng, st, p, tb, npr, rank, world, group=None):
     collective of 8 B per ray (RCCL over xGMI: 19 MB for C3, 77 MB for C5) --
     into ``(cost, frozen)`` over every ray, the same on every rank.  Without a
     group (a single-GPU rehearsal of one rank) every share is probed here.
-    A ray's probe is the same on any rank (rays are independent), so the costs
-    equal the unsharded probe's bit for bit."""
+    A ray's probe is the same on any rank (rays are independent), so a ray
+    live after the probe has the unsharded probe's cost bit for bit; a ray
+    frozen by then gets -1 (the unsharded path keeps its attempt count), and
+    ``cost_partition`` keys frozen rays as -1 either way, so the partition is
+    the same."""
     nray = st["nray"]
     dev = st["state"].device
     m = -(-nray // world)

@@ -163,17 +163,17 @@ def test_initial_rows_gpu_equals_host_full_c3(kind):
 
 
 # ------------------------------------------------------------------- T2 / T3
-def run_c2(kind, nt, chunk=None, order=None):
+def run_c2(kind, nt, chunk=None, order=None, eng=None, **kw):
     from engine import t_eval_of
     g = golden(f"init_C2_{kind}.npz")
-    eng = engine(kind)
+    eng = eng or engine(kind)
     y0 = torch.as_tensor(g["rows"][:5].reshape(5, -1))
     rows = {}
 
     def sink(i0, i1, out):
         rows[(i0, i1)] = out.cpu().numpy().copy()
 
-    res = eng.integrate(y0, nt, 7200.0, ttotal=(nt - 1) * 7200.0, chunk=chunk, sink=sink)
+    res = eng.integrate(y0, nt, 7200.0, ttotal=(nt - 1) * 7200.0, chunk=chunk, sink=sink, **kw)
     nray = y0.shape[1]
     hist = np.full((nray, nt, 8), np.nan)
     hist[:, 0, :7] = g["rows"].reshape(7, -1).T

@@ -86,6 +86,56 @@ def test_time_varying_c2_bitwise_with_oracle(fp32):
     assert np.array_equal(res.nacc.cpu().numpy(), nacc)
 
 
+# The time-varying kernels on a basic state held constant in time: one fp64
+# level (the C2 background, built on the device by rwrt_bs_ready) valid from
+# t0 = 1e9 s, so that every ray time lies before it and the time weight clips
+# to 0: g = g_0 (1 - 0) + g_0 0 == g_0 bit for bit (x + x * 0 == x for every
+# finite x, signed zeros included).  The reference integrates exactly that
+# state (fun ignores t, wr.py:784-789), so the rwrt_rk45_*_tv kernels --
+# 64 rays per wave (VaryingBG<double>: one level in the LDS cache, one
+# gathered), 32 (PairVaryingBG64: lane pairs), and the latency waves
+# (BlockVaryingBG<double>) -- must give the reference's own rows and
+# accepted-step counts ("reduce bitwise to the
+# reference for a constant-in-time background").
+TV_HELD = [(32, 0), (64, 0), (32, (64, 1))]
+
+
+def held_engine(kind, lanes):
+    import synthetic as S
+    from engine import RayEngine
+    from levels import Levels
+    b = S.background(kind)
+    lv = Levels(b["lat"], b["lon"], 1, t0=1e9, dt=6 * 3600.0)
+    lv.set_level(0, b["u"], b["v"])
+    eng = RayEngine.from_levels(lv, time_varying=True)
+    assert eng.bg is not None
+    eng.tv_lanes = lanes
+    return eng
+
+
+@pytest.mark.parametrize("lanes,team", TV_HELD, ids=["pair32", "lanes64", "latency_waves"])
+@pytest.mark.parametrize("kind", KINDS)
+def test_time_varying_kernels_held_state_equal_reference(kind, lanes, team):
+    from test_gpu_parity import bitwise, run_c2
+    eng = held_engine(kind, lanes)
+    kw = dict(order_policy="cell", first_chunk=[6], team=team) if team else {}
+    # the reference's own rows at 2 h, 1 d, 10 d and accepted steps (golden)
+    g = golden(f"traj_C2_{kind}.npz")
+    hist, res = run_c2(kind, int(g["nt"]), chunk=40 if team else None, eng=eng, **kw)
+    for j, row in enumerate(g["rows"]):
+        assert bitwise(hist[:, row, :7].T, g["hist"][:, j]), row
+    assert np.array_equal(res.nacc.cpu().numpy(), g["nacc"])
+    if team:
+        assert any(l["n_heavy"] for l in eng.launch_log), eng.launch_log
+    # every row of 90 days (the reference's arithmetic, oracle row hashes)
+    g = golden(f"ref90_C2_{kind}.npz")
+    nt = int(g["nt"])
+    hist, res = run_c2(kind, nt, chunk=120 if team else None, eng=eng, **kw)
+    hist = np.transpose(hist[:, :, :7], (2, 1, 0))
+    check_rows(row_hashes(hist), g["row_sha"], hist, g["last"])
+    assert np.array_equal(res.nacc.cpu().numpy(), g["nacc"])
+
+
 def test_interleaved_division_pair_is_ieee():
     """div2 (two IEEE divisions interleaved in inline asm) == a / b bit for bit,
     as either quotient of the pair, on random, extreme and special operands."""

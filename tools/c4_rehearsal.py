@@ -5,8 +5,9 @@
 
 ``--config C5`` splits BASELINE configs[4] instead (bench.py --config C5: the
 0.25-degree time-varying background, 361 levels, 9.67 M slots / 4.03 M live
-rays, the cell-ordered queue, 48-row launches for fp64 levels and 240 for
-fp32), the way ``bench.py --config C5 --gpus W`` splits it.
+rays, the cell-ordered queue, rows per launch from
+``bench.c5_rows_per_launch``), the way ``bench.py --config C5 --gpus W``
+splits it.
 
 For each world size W the C3 set is split exactly as ``bench.py --gpus W``
 splits it (shard.run_sharded: probe launch over every ray, snake deal by probe
@@ -78,7 +79,7 @@ def main():
     ap.add_argument("--config", default="C3", choices=["C3", "C5"])
     ap.add_argument("--fields", default="fp64", choices=["fp64", "fp32"], help="C5: level storage")
     ap.add_argument("--reps", type=int, default=2)
-    ap.add_argument("--chunk", type=int, default=0, help="C5: rows per launch (default: bench.py's, 48 fp64 / 240 fp32)")
+    ap.add_argument("--chunk", type=int, default=0, help="C5: rows per launch (default: bench.c5_rows_per_launch)")
     ap.add_argument("--shard-probe", type=int, default=1, choices=[0, 1],
                     help="each rank probes 1/W of the rays, costs all-gathered (bench.py's default)")
     a = ap.parse_args()
