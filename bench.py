@@ -494,10 +494,12 @@ def main():
     # this rank's rows stay in HBM (C3 on one GPU: 166 GB of 288 GB), so the
     # ray loop is a few launches: the probe, two short re-ordering launches,
     # then all the rest (ranks sharing a GPU share its memory)
-    n_local = nslot if weak else -(-nslot // world) + 2       # shard size bound (cost_partition)
+    # row blocks for the live rays only (rwrt_rk45_run_slots, ABI 4): this
+    # rank's live rays bound them (cost_partition deals the live rays snake-wise)
+    n_blk = n_live if weak else -(-n_live // world) + 2
     free = torch.cuda.mem_get_info(dev)[0] // share
-    chunk = args.chunk or max(1, min(nt - 1, int(0.8 * free) // (n_local * 64)))
-    out = torch.empty((n_local, min(chunk, nt - 1), 8), dtype=torch.float64, device=dev)
+    chunk = args.chunk or max(1, min(nt - 1, int(0.8 * free) // (max(n_blk, 1) * 64)))
+    out = torch.empty((max(n_blk, 1), min(chunk, nt - 1), 8), dtype=torch.float64, device=dev)
     lead = [int(x) for x in str(args.first_chunk).split(",") if x]
     team = (args.team if args.team == "auto" else
             [x if x == "auto" else int(x) for x in args.team.split(",")] if "," in args.team else int(args.team))
@@ -610,6 +612,10 @@ def main():
                        "parallelism": par},
             "ray_steps_per_step": tot_steps / args.steps,
             "ray_steps_per_step_rank0": steps_done / args.steps,
+            "rows_bytes": {"rank0": int(eng.rows_bytes),
+                           "dense_equivalent": int(r.idx.numel()) * min(chunk, nt - 1) * 64,
+                           "note": "rank 0's device row buffer: row blocks for the rays live at a launch's "
+                                   "start only (rwrt_rk45_run_slots); frozen rays' rows are tails"},
             "rejected_per_accepted": tot_rej * args.steps / max(tot_steps, 1),
             "host_init_s": t_init,
             "init": ("GPU rwrt_ray_initial inside every timed step (bit-identical to the host rows)"
@@ -807,11 +813,12 @@ def main_c5(args, dist, group, rank, world, dev, share=1):
     nslot = y0.shape[1]
     n_live = int((~torch.isnan(y0.sum(0))).sum().item())
     # rows per launch: c5_rows_per_launch, capped by the row buffer's memory
-    n_local = nslot if weak else -(-nslot // world) + 2
+    # (row blocks for the live rays only, as for C3)
+    n_blk = n_live if weak else -(-n_live // world) + 2
     free = torch.cuda.mem_get_info(dev)[0] // share
-    cap = max(1, min(nt - 1, int(0.8 * free) // (n_local * 64)))
+    cap = max(1, min(nt - 1, int(0.8 * free) // (max(n_blk, 1) * 64)))
     chunk = min(args.chunk or c5_rows_per_launch(lv.fp32, 1 if weak else world, nt), cap)
-    out = torch.empty((n_local, min(chunk, nt - 1), 8), dtype=torch.float64, device=dev)
+    out = torch.empty((max(n_blk, 1), min(chunk, nt - 1), 8), dtype=torch.float64, device=dev)
     lead = [int(x) for x in str(args.first_chunk).split(",") if x]
     # latency mode (the time-varying latency waves: one ray per wave on its 64
     # lanes, BlockVaryingBG) for a split set's heaviest rays; one GPU's set is
@@ -885,6 +892,8 @@ def main_c5(args, dist, group, rank, world, dev, share=1):
             "latency_mode": (f"{team if team == 'auto' else team} (time-varying latency waves: one ray per wave "
                              f"on its 64 lanes, BlockVaryingBG)" if team else "none"),
             "launches": [dict(d) for d in eng.launch_log],
+            "rows_bytes": {"rank0": int(eng.rows_bytes),
+                           "note": "rank 0's device row buffer (row blocks for live rays only, ABI 4)"},
             "ray_steps_per_step": tot_steps / args.steps,
             "rejected_per_accepted": tot_rej * args.steps / max(tot_steps, 1),
             "levels_build_s": t_build,

@@ -33,7 +33,8 @@
 extern "C" {
 #endif
 
-#define RWRT_ABI_VERSION 3  /* 3: constant row tails (rwrt_rk45_run_tails, rwrt_expand_tails) */
+#define RWRT_ABI_VERSION 4  /* 3: constant row tails (rwrt_rk45_run_tails, rwrt_expand_tails);
+                               4: row blocks for the live rays only (rwrt_rk45_run_slots) */
 #define RWRT_NFIELD_REF 18  /* BS.fields[..., 18]            (bs.py:349-368) */
 #define RWRT_NFIELD_PACK 12 /* 11 hot fields + 1 pad per grid point           */
 #define RWRT_NVAR 5         /* y = (lon, lat, k, l, amp)     (wr.py:768-776)  */
@@ -244,6 +245,33 @@ rwrt_status rwrt_expand_tails(int64_t nray, int32_t it_begin, int32_t it_end,
                               const int32_t* d_tail_from, const double* d_tail_row,
                               double* d_out, void* stream);
 
+/* ABI 4: rows only for the rays live at the call's start.  rwrt_row_slots
+ * numbers the rays whose state has a finite mean (rkf45.py:400-403: the rays
+ * a call steps; every other ray repeats one row, its tail) in ray order:
+ *  d_row_slot[nray] (int32) := j's index among them, -1 for a frozen ray;
+ *  d_nslot[0] (int64) := their number.
+ * rwrt_rk45_run_slots is rwrt_rk45_run_tails with ray j's rows at
+ * d_out[(d_row_slot[j]*(it_end-it_begin) + r)*8 + 0..7]: d_out holds
+ * nslot x rows x 8 doubles instead of nray x rows x 8 (C3: the 716 400 live
+ * rays of 2.40 M slots, 49.5 GB instead of 166 GB for a 1 080-row call).
+ * d_row_slot must come from rwrt_row_slots on the call's own d_state (after
+ * the previous call); tails are required.  rwrt_expand_slots writes the dense
+ * rows d_out[nray][rows][8] of such a call from its row blocks d_rows and its
+ * tails: equal bit for bit to rwrt_rk45_run's d_out. */
+rwrt_status rwrt_row_slots(int64_t nray, const double* d_state, int32_t* d_row_slot, int64_t* d_nslot,
+                           void* stream);
+rwrt_status rwrt_rk45_run_slots(rwrt_ctx* ctx, const rwrt_grid* g, const double* d_packed,
+                                int64_t nray, const rwrt_params* p,
+                                const double* d_tbound, int32_t it_begin,
+                                int32_t it_end, const int64_t* d_order,
+                                int64_t n_heavy, double* d_state, int64_t* d_count,
+                                int32_t* d_nanrow, double* d_out, const int32_t* d_row_slot,
+                                int32_t* d_tail_from, double* d_tail_row, int32_t* d_work,
+                                void* stream);
+rwrt_status rwrt_expand_slots(int64_t nray, int32_t it_begin, int32_t it_end, const int32_t* d_row_slot,
+                              const int32_t* d_tail_from, const double* d_tail_row, const double* d_rows,
+                              double* d_out, void* stream);
+
 /* Fixed-step RK4 ray loop, the reference's default integrator:
  * WR.core_ray_run_numpy (wr.py:702-765) with rk4_step_numpy (wr.py:583-622)
  * and core_rk4_step (wr.py:89-95), for rows it_begin <= i < it_end, dt =
@@ -305,6 +333,15 @@ rwrt_status rwrt_rk45_run_tv_tails(rwrt_ctx* ctx, const rwrt_grid* g, const rwrt
                                    int64_t n_heavy, double* d_state, int64_t* d_count,
                                    int32_t* d_nanrow, double* d_out, int32_t* d_tail_from,
                                    double* d_tail_row, int32_t* d_work, void* stream);
+/* rwrt_rk45_run_tv with row blocks for the live rays only (as rwrt_rk45_run_slots). */
+rwrt_status rwrt_rk45_run_tv_slots(rwrt_ctx* ctx, const rwrt_grid* g, const rwrt_background* b,
+                                   int64_t nray, const rwrt_params* p,
+                                   const double* d_tbound, int32_t it_begin,
+                                   int32_t it_end, const int64_t* d_order,
+                                   int64_t n_heavy, double* d_state, int64_t* d_count,
+                                   int32_t* d_nanrow, double* d_out, const int32_t* d_row_slot,
+                                   int32_t* d_tail_from, double* d_tail_row, int32_t* d_work,
+                                   void* stream);
 /* The time-varying RHS at per-point times: d_t[n], d_y[5][n] -> d_dydt[5][n]. */
 rwrt_status rwrt_rhs_tv(const rwrt_grid* g, const rwrt_background* b, int64_t n,
                         const double* d_t, const double* d_y, double* d_dydt,

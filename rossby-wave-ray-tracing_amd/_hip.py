@@ -18,9 +18,10 @@ ABI_SYMBOLS = ("rwrt_version", "rwrt_last_error", "rwrt_ctx_create", "rwrt_ctx_d
                "rwrt_pack_fields",
                "rwrt_mercator_point", "rwrt_rhs", "rwrt_dp54_attempt",
                "rwrt_ray_initial", "rwrt_rk45_init", "rwrt_rk45_run", "rwrt_rk45_run_tails",
-               "rwrt_expand_tails", "rwrt_rk4_run",
+               "rwrt_expand_tails", "rwrt_row_slots", "rwrt_rk45_run_slots", "rwrt_expand_slots",
+               "rwrt_rk4_run",
                "rwrt_bs_ready", "rwrt_rk45_init_tv", "rwrt_rk45_run_tv", "rwrt_rk45_run_tv_tails",
-               "rwrt_rhs_tv",
+               "rwrt_rk45_run_tv_slots", "rwrt_rhs_tv",
                "rwrt_kat_rk45", "rwrt_selftest_math", "rwrt_host_fill_rows")
 
 RWRT_OK, RWRT_ERR_ARG, RWRT_ERR_HIP, RWRT_SOLVER_FAILED = 0, 1, 2, 3
@@ -82,12 +83,18 @@ def load():
         "rwrt_rk45_run_tails": [_P, G, _P, _I64, Pr, _P, _I32, _I32, _P, _I64, _P, _P, _P, _P, _P, _P, _P,
                                 _P],
         "rwrt_expand_tails": [_I64, _I32, _I32, _P, _P, _P, _P],
+        "rwrt_row_slots": [_I64, _P, _P, _P, _P],
+        "rwrt_rk45_run_slots": [_P, G, _P, _I64, Pr, _P, _I32, _I32, _P, _I64, _P, _P, _P, _P, _P, _P, _P,
+                                _P, _P],
+        "rwrt_expand_slots": [_I64, _I32, _I32, _P, _P, _P, _P, _P, _P],
         "rwrt_rk4_run": [_P, G, _P, _I64, Pr, _I32, _I32, _P, _P, _P, _P, _P, _P, _P],
         "rwrt_bs_ready": [_I32, _I32, _P, _P, _P, _D, _D, _P, _P, _I32, _P],
         "rwrt_rk45_init_tv": [G, B, _I64, _P, Pr, _P, _P, _P, _P, _P, _P],
         "rwrt_rk45_run_tv": [_P, G, B, _I64, Pr, _P, _I32, _I32, _P, _I64, _P, _P, _P, _P, _P, _P],
         "rwrt_rk45_run_tv_tails": [_P, G, B, _I64, Pr, _P, _I32, _I32, _P, _I64, _P, _P, _P, _P, _P, _P, _P,
                                    _P],
+        "rwrt_rk45_run_tv_slots": [_P, G, B, _I64, Pr, _P, _I32, _I32, _P, _I64, _P, _P, _P, _P, _P, _P, _P,
+                                   _P, _P],
         "rwrt_ctx_create": [_I32, ctypes.POINTER(_P)],
         "rwrt_ctx_destroy": [_P],
         "rwrt_ctx_set_latency_density": [_P, _I32],

@@ -2323,7 +2323,19 @@ struct RunArgs {
   int32_t quad_per_wave = 16;  // latency mode: rays per wave (1..16; fewer = less divergence per ray)
   int64_t* trace = nullptr;    // diagnostic ray trace (rwrt_ctx_set_trace), positions < trace_cap
   int64_t trace_cap = 0;
+  // ABI 4 (rwrt_rk45_run_slots): the row block of ray j in out is
+  // row_slot[j] (the rays live at the call's start, numbered in ray order by
+  // rwrt_row_slots; -1 for a frozen ray, whose rows are its tail); NULL: j
+  const int32_t* row_slot = nullptr;
 };
+
+// The first output row of ray `ray` in this call's row buffer (NULL when the
+// ray has no row block: frozen at the call's start, so never stepped here)
+template <class BG>
+__device__ __forceinline__ double* row_block(const RunArgs<BG>& a, int64_t ray) {
+  const int64_t slot = a.row_slot ? (int64_t)a.row_slot[ray] : ray;
+  return slot < 0 ? nullptr : a.out + (size_t)slot * (size_t)(a.it_end - a.it_begin) * RWRT_NOUT;
+}
 
 
 // A frozen ray's rows are all one row (rkf45.py:400-403: its state never
@@ -2673,7 +2685,6 @@ __device__ __forceinline__ void quad_rays(const RunArgs<StaticBG>& a, char* cach
   R.odd = (R.role & 1) != 0;
   R.high = (R.role & 2) != 0;
   KQuad K{Kq + threadIdx.x};
-  const int64_t nrows = a.it_end - a.it_begin;
   // order position of this quad's ray, a.quad_per_wave quads per wave
   const int qi = (threadIdx.x & 63) >> 2;
   // consecutive positions share a wave (p -> wave p / quad_per_wave): rays of
@@ -2698,6 +2709,7 @@ __device__ __forceinline__ void quad_rays(const RunArgs<StaticBG>& a, char* cach
   double t = a.state[10 * a.nray + ray], habs = a.state[11 * a.nray + ray], hs = 0.0;
   int64_t nacc = a.count[2 * ray], nrej = a.count[2 * ray + 1];
   const int64_t att0 = nacc + nrej;
+  double* const rows = row_block(a, ray);
   if (kTrace && w < a.trace_cap && R.role == 0) trace_start(a.trace, w);
   int32_t nanrow = a.nanrow[ray];
   int32_t it = a.it_begin;
@@ -2777,11 +2789,11 @@ __device__ __forceinline__ void quad_rays(const RunArgs<StaticBG>& a, char* cach
       ugvg_at(a.B, tb, y[0], y[1], y[2], y[3], ug, vg);
     }
     const int last = (st == 2) ? a.it_end : it + 1;
-    if (writer) {
+    if (writer && rows) {
       const double2 r0 = make_double2(y[0], y[1]), r1 = make_double2(y[2], y[3]);
       const double2 r2 = make_double2(y[4], ug), r3 = make_double2(vg, (double)nacc);
       for (int kr = it; kr < last; ++kr) {
-        double2* o = reinterpret_cast<double2*>(a.out + ((size_t)ray * nrows + (kr - a.it_begin)) * RWRT_NOUT);
+        double2* o = reinterpret_cast<double2*>(rows + (size_t)(kr - a.it_begin) * RWRT_NOUT);
         store_row16<RWRT_ROW_NT>(o + 0, r0);
         store_row16<RWRT_ROW_NT>(o + 1, r1);
         store_row16<RWRT_ROW_NT>(o + 2, r2);
@@ -2845,11 +2857,11 @@ __device__ __forceinline__ void run_rays(const RunArgs<BG>& a, const LBG& lbg, c
   const RayProblem P{lbg};
   // (a latency wave's lane 0 stores; lane pairs: the lower lane)
   const bool writer = kReplica ? (threadIdx.x & 63u) == 0 : kPair ? (threadIdx.x & 63u) < 32u : true;
-  const int64_t nrows = a.it_end - a.it_begin;
   Lane<RayProblem, KStore> L;
   L.K.p = reinterpret_cast<double*>(smem) + threadIdx.x;
   L.K.stride = 256;
   int64_t ray = -1, nacc = 0, nrej = 0;
+  double* rows = nullptr;   // the ray's row block (row_block)
   int32_t it = 0, nanrow = 0, wpos = 0;   // (wpos: the ray's queue position, kTrace only)
   double prev_lon = 0.0, prev_lat = 0.0, cos_prev = 0.0;
   // above frozen_fill_kernel's waves (priority 0) sharing the SIMD: the
@@ -2886,6 +2898,7 @@ __device__ __forceinline__ void run_rays(const RunArgs<BG>& a, const LBG& lbg, c
       }
       L.t = a.state[10 * a.nray + ray];
       L.habs = a.state[11 * a.nray + ray];
+      rows = row_block(a, ray);
       L.in_step = false;
       L.rejected = false;
       L.hs = 0.0;
@@ -2942,20 +2955,17 @@ __device__ __forceinline__ void run_rays(const RunArgs<BG>& a, const LBG& lbg, c
     // masks against itself is a no-op), so every remaining row of the chunk
     // equals this one: write them all and release the lane.
     const int last = (st == Lane<RayProblem, KStore>::kFrozen) ? a.it_end : it + 1;
-    if (writer) {
-      // non-temporal, like the fill's: the rows stream past the L2 that
-      // holds the basic state (+0.5 % on C3, profiles/r3/sched/pass_aa_nt_rows.txt;
-      // no row stores at all would be +3.3 %)
-      double2* o = reinterpret_cast<double2*>(a.out + ((size_t)ray * nrows + (it - a.it_begin)) * RWRT_NOUT);
+    if (writer && rows) {
+      double2* o = reinterpret_cast<double2*>(rows + (size_t)(it - a.it_begin) * RWRT_NOUT);
       store_row16<RWRT_ROW_NT>(o + 0, r0);
       store_row16<RWRT_ROW_NT>(o + 1, r1);
       store_row16<RWRT_ROW_NT>(o + 2, r2);
       store_row16<RWRT_ROW_NT>(o + 3, r3);
     }
-    if (RARE(last > it + 1) && writer) {
+    if (RARE(last > it + 1) && writer && rows) {
       asm volatile("");   // frozen: the remaining rows of the chunk (rare branch)
       for (int k = it + 1; k < last; ++k) {
-        double2* o = reinterpret_cast<double2*>(a.out + ((size_t)ray * nrows + (k - a.it_begin)) * RWRT_NOUT);
+        double2* o = reinterpret_cast<double2*>(rows + (size_t)(k - a.it_begin) * RWRT_NOUT);
         o[0] = r0;
         o[1] = r1;
         o[2] = r2;
@@ -3722,7 +3732,7 @@ rwrt_status launch_run(rwrt_ctx* ctx, const BG& B, int64_t nray, const rwrt_para
                        const double* d_tbound, int32_t it_begin, int32_t it_end,
                        const int64_t* d_order, int64_t n_heavy, double* d_state, int64_t* d_count,
                        int32_t* d_nanrow, double* d_out, int32_t* d_tail_from, double* d_tail_row,
-                       int32_t* d_work, void* stream) {
+                       int32_t* d_work, void* stream, const int32_t* d_row_slot = nullptr) {
   if (rwrt_status s = ctx_check(ctx)) return s;
   if (!p) return fail(RWRT_ERR_ARG, "params is NULL%s");
   if (nray < 0 || nray > 0x7fffffffLL) return fail(RWRT_ERR_ARG, "nray out of range%s");
@@ -3735,6 +3745,8 @@ rwrt_status launch_run(rwrt_ctx* ctx, const BG& B, int64_t nray, const rwrt_para
   if (!d_tail_from != !d_tail_row) return fail(RWRT_ERR_ARG, "tails need both d_tail_from and d_tail_row%s");
   if (reinterpret_cast<uintptr_t>(d_tail_row) % 16 != 0)
     return fail(RWRT_ERR_ARG, "tail rows must be 16-byte aligned%s");
+  if (d_row_slot && !d_tail_from)
+    return fail(RWRT_ERR_ARG, "row slots need tails (the rays without a slot keep theirs there)%s");
   if (nray == 0) return RWRT_OK;
   if (n_heavy < 0 || n_heavy > nray) return fail(RWRT_ERR_ARG, "n_heavy out of range%s");
   if (n_heavy > 0 && !d_order) return fail(RWRT_ERR_ARG, "n_heavy > 0 needs d_order%s");
@@ -3770,6 +3782,7 @@ rwrt_status launch_run(rwrt_ctx* ctx, const BG& B, int64_t nray, const rwrt_para
   RunArgs<BG> a{B, nray, p->rtol, p->atol, p->min_step, p->cut_off, p->nt, it_begin, it_end,
                 d_tbound, d_order, d_state, d_count, d_nanrow, d_out, d_work,
                 n_heavy, 0, haversine_cut(p->cut_off), nullptr};
+  a.row_slot = d_row_slot;
   // frozen rays: flagged on `stream`, filled on the context's side stream
   // while the run kernel (which skips them) integrates the rest; `stream` then
   // waits for the fill, so the call stays one stream-ordered operation.  With
@@ -3971,6 +3984,100 @@ __global__ void expand_tails_kernel(double* __restrict__ out, int64_t nray, int3
   }
 }
 
+// rwrt_expand_slots: ray j's rows from its row block (compact rows of a
+// rwrt_rk45_run_slots call) below tail_from[j], its tail row from there on
+__global__ void expand_slots_kernel(double* __restrict__ out, int64_t nray, int32_t it_begin, int32_t nrows,
+                                    const int32_t* __restrict__ row_slot, const int32_t* __restrict__ tail_from,
+                                    const double* __restrict__ tail_row, const double* __restrict__ rows) {
+  const int64_t per = (int64_t)nrows * 4, n = nray * per;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t j = i / per;
+    const int64_t q = i - j * per;
+    const int32_t sl = row_slot[j];
+    if (it_begin + (int32_t)(q >> 2) >= tail_from[j])
+      reinterpret_cast<double2*>(out)[i] = reinterpret_cast<const double2*>(tail_row)[j * 4 + (q & 3)];
+    else if (sl >= 0)
+      reinterpret_cast<double2*>(out)[i] = reinterpret_cast<const double2*>(rows)[(int64_t)sl * per + q];
+  }
+}
+
+// rwrt_row_slots: the rays live at this point (finite state mean, the run
+// kernels' frozen test) numbered in ray order -- an exclusive scan of the
+// live flags over tiles of kSlotTile rays: per-tile counts (parked in each
+// tile's first row_slot entry), one block scans them into offsets, then each
+// tile numbers its rays (wave ballots).  No scratch beyond row_slot itself.
+constexpr int kSlotTile = 4096;   // 256 threads x 16 rays
+__device__ __forceinline__ bool slot_live(const double* __restrict__ state, int64_t nray, int64_t i) {
+  double sum = state[i];
+#pragma unroll
+  for (int v = 1; v < 5; ++v) sum = sum + state[v * nray + i];
+  return !isnan(sum / 5.0);   // frozen_flag_kernel's test
+}
+__global__ void __launch_bounds__(256) slot_count_kernel(const double* __restrict__ state, int64_t nray,
+                                                         int32_t* __restrict__ row_slot) {
+  const int64_t base = (int64_t)blockIdx.x * kSlotTile;
+  int c = 0;
+  for (int k = 0; k < kSlotTile / 256; ++k) {
+    const int64_t i = base + k * 256 + threadIdx.x;
+    c += (i < nray && slot_live(state, nray, i)) ? 1 : 0;
+  }
+  __shared__ int part[4];
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) row_slot[base] = part[0] + part[1] + part[2] + part[3];
+}
+__global__ void __launch_bounds__(1024) slot_offsets_kernel(int64_t nray, int32_t* __restrict__ row_slot,
+                                                            int64_t* __restrict__ nslot) {
+  const int64_t tiles = (nray + kSlotTile - 1) / kSlotTile;
+  __shared__ int wsum[16];
+  __shared__ int carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int64_t t0 = 0; t0 < tiles; t0 += 1024) {
+    const int64_t t = t0 + threadIdx.x;
+    const int v = t < tiles ? row_slot[t * kSlotTile] : 0;
+    int x = v;   // inclusive scan within the wave
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(x, o);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    int before = carry;
+    for (int w = 0; w < wave; ++w) before += wsum[w];
+    if (t < tiles) row_slot[t * kSlotTile] = before + x - v;   // exclusive
+    __syncthreads();
+    if (threadIdx.x == 1023) carry = before + x;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *nslot = carry;
+}
+__global__ void __launch_bounds__(256) slot_assign_kernel(const double* __restrict__ state, int64_t nray,
+                                                          int32_t* __restrict__ row_slot) {
+  const int64_t base = (int64_t)blockIdx.x * kSlotTile;
+  __shared__ int off;
+  __shared__ int wcnt[4];
+  if (threadIdx.x == 0) off = row_slot[base];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int k = 0; k < kSlotTile / 256; ++k) {
+    const int64_t i = base + k * 256 + threadIdx.x;
+    const bool live = i < nray && slot_live(state, nray, i);
+    const uint64_t m = __ballot(live);
+    if (lane == 0) wcnt[wave] = __popcll(m);
+    __syncthreads();
+    int before = off;
+    for (int w = 0; w < wave; ++w) before += wcnt[w];
+    const int mine = before + __popcll(m & ((1ull << lane) - 1ull));
+    if (i < nray) row_slot[i] = live ? mine : -1;
+    __syncthreads();
+    if (threadIdx.x == 0) off += wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+    __syncthreads();
+  }
+}
+
 // rwrt_selftest_math kinds 36/37: the jump mask's verdict (1: jump) for a step
 // of (dlat, dlon) = (x, y) from (lon, lat) = (1.0, 0.6), cut_off 0.05 rad:
 // 36 with the ray loops' polynomial "no jump" shortcut, 37 without it.
@@ -4165,6 +4272,51 @@ rwrt_status rwrt_rk45_run_tails(rwrt_ctx* ctx, const rwrt_grid* g, const double*
                     d_count, d_nanrow, d_out, d_tail_from, d_tail_row, d_work, stream);
 }
 
+rwrt_status rwrt_rk45_run_slots(rwrt_ctx* ctx, const rwrt_grid* g, const double* d_packed,
+                                int64_t nray, const rwrt_params* p, const double* d_tbound,
+                                int32_t it_begin, int32_t it_end, const int64_t* d_order,
+                                int64_t n_heavy, double* d_state, int64_t* d_count, int32_t* d_nanrow,
+                                double* d_out, const int32_t* d_row_slot, int32_t* d_tail_from,
+                                double* d_tail_row, int32_t* d_work, void* stream) {
+  if (!d_row_slot) return fail(RWRT_ERR_ARG, "rwrt_rk45_run_slots needs d_row_slot%s");
+  Field F;
+  if (rwrt_status s = make_field(g, d_packed, F)) return s;
+  return launch_run(ctx, StaticBG{F}, nray, p, d_tbound, it_begin, it_end, d_order, n_heavy, d_state,
+                    d_count, d_nanrow, d_out, d_tail_from, d_tail_row, d_work, stream, d_row_slot);
+}
+
+rwrt_status rwrt_row_slots(int64_t nray, const double* d_state, int32_t* d_row_slot, int64_t* d_nslot,
+                           void* stream) {
+  if (nray < 0 || nray > 0x7fffffffLL) return fail(RWRT_ERR_ARG, "nray out of range%s");
+  if (!d_nslot || (nray > 0 && (!d_state || !d_row_slot))) return fail(RWRT_ERR_ARG, "NULL buffer to rwrt_row_slots%s");
+  hipStream_t st = (hipStream_t)stream;
+  if (nray == 0) {
+    if (hipMemsetAsync(d_nslot, 0, sizeof(int64_t), st) != hipSuccess) return check_launch("hipMemsetAsync(nslot)");
+    return RWRT_OK;
+  }
+  const int64_t tiles = (nray + kSlotTile - 1) / kSlotTile;
+  hipLaunchKernelGGL(slot_count_kernel, dim3((unsigned)tiles), dim3(256), 0, st, d_state, nray, d_row_slot);
+  hipLaunchKernelGGL(slot_offsets_kernel, dim3(1), dim3(1024), 0, st, nray, d_row_slot, d_nslot);
+  hipLaunchKernelGGL(slot_assign_kernel, dim3((unsigned)tiles), dim3(256), 0, st, d_state, nray, d_row_slot);
+  return check_launch("row slot kernels");
+}
+
+rwrt_status rwrt_expand_slots(int64_t nray, int32_t it_begin, int32_t it_end, const int32_t* d_row_slot,
+                              const int32_t* d_tail_from, const double* d_tail_row, const double* d_rows,
+                              double* d_out, void* stream) {
+  if (nray < 0 || it_begin >= it_end) return fail(RWRT_ERR_ARG, "bad rwrt_expand_slots shape%s");
+  if (nray == 0) return RWRT_OK;
+  if (!d_row_slot || !d_tail_from || !d_tail_row || !d_rows || !d_out)
+    return fail(RWRT_ERR_ARG, "NULL buffer to rwrt_expand_slots%s");
+  if (reinterpret_cast<uintptr_t>(d_out) % 16 != 0 || reinterpret_cast<uintptr_t>(d_tail_row) % 16 != 0 ||
+      reinterpret_cast<uintptr_t>(d_rows) % 16 != 0)
+    return fail(RWRT_ERR_ARG, "rows must be 16-byte aligned%s");
+  const int64_t n = nray * (int64_t)(it_end - it_begin) * 4;
+  hipLaunchKernelGGL(expand_slots_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, d_out,
+                     nray, it_begin, it_end - it_begin, d_row_slot, d_tail_from, d_tail_row, d_rows);
+  return check_launch("expand_slots_kernel");
+}
+
 rwrt_status rwrt_expand_tails(int64_t nray, int32_t it_begin, int32_t it_end, const int32_t* d_tail_from,
                               const double* d_tail_row, double* d_out, void* stream) {
   if (nray < 0 || it_begin >= it_end) return fail(RWRT_ERR_ARG, "bad rwrt_expand_tails shape%s");
@@ -4206,22 +4358,23 @@ rwrt_status rwrt_rk45_run_tv(rwrt_ctx* ctx, const rwrt_grid* g, const rwrt_backg
                                 d_count, d_nanrow, d_out, nullptr, nullptr, d_work, stream);
 }
 
-rwrt_status rwrt_rk45_run_tv_tails(rwrt_ctx* ctx, const rwrt_grid* g, const rwrt_background* b,
+static rwrt_status run_tv(rwrt_ctx* ctx, const rwrt_grid* g, const rwrt_background* b,
                                    int64_t nray, const rwrt_params* p, const double* d_tbound,
                                    int32_t it_begin, int32_t it_end, const int64_t* d_order, int64_t n_heavy,
                                    double* d_state, int64_t* d_count, int32_t* d_nanrow, double* d_out,
-                                   int32_t* d_tail_from, double* d_tail_row, int32_t* d_work, void* stream) {
+                                   int32_t* d_tail_from, double* d_tail_row, int32_t* d_work, void* stream,
+                          const int32_t* d_row_slot) {
   if (b && b->fp32 == 2) {
     VaryingBGA32 B;
     if (rwrt_status s = make_varying(g, b, static_cast<VaryingBG<float>&>(B))) return s;
     return launch_run(ctx, B, nray, p, d_tbound, it_begin, it_end, d_order, n_heavy, d_state, d_count,
-                      d_nanrow, d_out, d_tail_from, d_tail_row, d_work, stream);
+                      d_nanrow, d_out, d_tail_from, d_tail_row, d_work, stream, d_row_slot);
   }
   if (b && b->fp32) {
     VaryingBG<float> B;
     if (rwrt_status s = make_varying(g, b, B)) return s;
     return launch_run(ctx, B, nray, p, d_tbound, it_begin, it_end, d_order, n_heavy, d_state, d_count,
-                      d_nanrow, d_out, d_tail_from, d_tail_row, d_work, stream);
+                      d_nanrow, d_out, d_tail_from, d_tail_row, d_work, stream, d_row_slot);
   }
   int lanes = 64;
   if (ctx) {
@@ -4232,7 +4385,27 @@ rwrt_status rwrt_rk45_run_tv_tails(rwrt_ctx* ctx, const rwrt_grid* g, const rwrt
   if (rwrt_status s = make_varying(g, b, B)) return s;
   B.half = lanes == 32;
   return launch_run(ctx, B, nray, p, d_tbound, it_begin, it_end, d_order, n_heavy, d_state, d_count,
-                    d_nanrow, d_out, d_tail_from, d_tail_row, d_work, stream);
+                    d_nanrow, d_out, d_tail_from, d_tail_row, d_work, stream, d_row_slot);
+}
+
+rwrt_status rwrt_rk45_run_tv_tails(rwrt_ctx* ctx, const rwrt_grid* g, const rwrt_background* b,
+                                   int64_t nray, const rwrt_params* p, const double* d_tbound,
+                                   int32_t it_begin, int32_t it_end, const int64_t* d_order, int64_t n_heavy,
+                                   double* d_state, int64_t* d_count, int32_t* d_nanrow, double* d_out,
+                                   int32_t* d_tail_from, double* d_tail_row, int32_t* d_work, void* stream) {
+  return run_tv(ctx, g, b, nray, p, d_tbound, it_begin, it_end, d_order, n_heavy, d_state, d_count, d_nanrow,
+                d_out, d_tail_from, d_tail_row, d_work, stream, nullptr);
+}
+
+rwrt_status rwrt_rk45_run_tv_slots(rwrt_ctx* ctx, const rwrt_grid* g, const rwrt_background* b,
+                                   int64_t nray, const rwrt_params* p, const double* d_tbound,
+                                   int32_t it_begin, int32_t it_end, const int64_t* d_order, int64_t n_heavy,
+                                   double* d_state, int64_t* d_count, int32_t* d_nanrow, double* d_out,
+                                   const int32_t* d_row_slot, int32_t* d_tail_from, double* d_tail_row,
+                                   int32_t* d_work, void* stream) {
+  if (!d_row_slot) return fail(RWRT_ERR_ARG, "rwrt_rk45_run_tv_slots needs d_row_slot%s");
+  return run_tv(ctx, g, b, nray, p, d_tbound, it_begin, it_end, d_order, n_heavy, d_state, d_count, d_nanrow,
+                d_out, d_tail_from, d_tail_row, d_work, stream, d_row_slot);
 }
 
 rwrt_status rwrt_rhs_tv(const rwrt_grid* g, const rwrt_background* b, int64_t n,

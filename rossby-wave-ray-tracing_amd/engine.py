@@ -71,9 +71,52 @@ class Tails:
         return torch.where((self.frm < i1)[:, None], self.row, view[:, -1])
 
 
-def deliver(eng, sink, i0, i1, view, tails):
+class Slots:
+    """The row blocks of one ``rwrt_rk45_run_slots`` launch (ABI 4): ray j's
+    rows are block ``slot[j]`` of the launch's row buffer, -1 for a ray frozen
+    at the launch's start (its rows are its tail).  ``n``: the blocks the first
+    launch of a run needs (later launches need no more: a frozen ray stays
+    frozen, rkf45.py:400-403)."""
+
+    def __init__(self, nray, device):
+        self.slot = torch.empty(nray, dtype=torch.int32, device=device)
+        self.n_dev = torch.zeros(1, dtype=torch.int64, device=device)
+        self.n = None
+
+    def compute(self, st, stream):
+        """Number the rays of ``st`` live now (``rwrt_row_slots``, async)."""
+        H.check(H.load().rwrt_row_slots(st["nray"], H.dptr(st["state"]), H.dptr(self.slot, torch.int32),
+                                        H.dptr(self.n_dev, torch.int64), stream))
+        return self
+
+    def count(self):
+        """The number of live rays (waits for ``compute``)."""
+        self.n = int(self.n_dev.item())
+        return self.n
+
+    def last_row(self, view, tails, i1):
+        """Each ray's last row of the launch ``[i0, i1)`` (row blocks ``view``)."""
+        blk = view[self.slot.clamp(min=0).to(torch.int64), -1] if view.shape[0] else tails.row
+        return torch.where((tails.frm < i1)[:, None], tails.row, blk)
+
+    def dense(self, view, tails, i0, i1, out=None):
+        """The launch's rows ``[nray, i1-i0, 8]`` made dense (``rwrt_expand_slots``)."""
+        nray = self.slot.numel()
+        if out is None or out.numel() < nray * (i1 - i0) * H.NOUT:
+            out = torch.empty((nray, i1 - i0, H.NOUT), dtype=F64, device=self.slot.device)
+        d = out.reshape(-1)[: nray * (i1 - i0) * H.NOUT].view(nray, i1 - i0, H.NOUT)
+        H.check(H.load().rwrt_expand_slots(nray, int(i0), int(i1), H.dptr(self.slot, torch.int32),
+                                           H.dptr(tails.frm, torch.int32), H.dptr(tails.row, F64),
+                                           H.dptr(view, F64), H.dptr(d, F64), H.stream(self.slot.device)))
+        return d
+
+
+def deliver(eng, sink, i0, i1, view, tails, slots=None):
     """Hand a launch's rows to ``sink``: with its tails when the sink takes
-    them (``sink.takes_tails``), else dense (the tails expanded into ``view``)."""
+    them (``sink.takes_tails``), else dense (the tails expanded into ``view``);
+    row blocks (``slots``) go only to a sink that takes them."""
+    if slots is not None:
+        return sink(i0, i1, view, tails, slots)
     if tails is not None and getattr(sink, "takes_tails", False):
         return sink(i0, i1, view, tails)
     if tails is not None:
@@ -94,6 +137,11 @@ class RayEngine:
     # only.  32: C5 1.17 -> 1.24e9 on one GPU, 8 shards 1.42 -> 0.78 s
     # (with the split set's long launches, bench.c5_rows_per_launch)
     tv_lanes = int(os.environ.get("RWRT_TV_LANES", "32"))
+    # row blocks for the live rays only (rwrt_rk45_run_slots, ABI 4): a launch
+    # whose rows go to a sink that takes them (``sink.takes_slots``), or to no
+    # one, gets a row buffer of live rays x rows instead of every slot x rows
+    # (C3: 49.5 GB instead of 166 GB); other sinks get dense rows as before
+    use_slots = os.environ.get("RWRT_SLOTS", "1") != "0"
 
     def __init__(self, fields, lon, lat, device=None):
         """``fields``: the reference stack ``[nlon(+1), nlat, 18]`` (numpy or tensor);
@@ -115,6 +163,7 @@ class RayEngine:
     bg = None   # rwrt_background of a time-varying state (None: the reference's static state)
     split_rho = None   # the last advance()'s rank correlation of its leading launches (split="auto")
     launch_log = ()    # the last advance()'s launches: rows and latency-mode decision
+    rows_bytes = 0     # the last advance()'s row buffers (device bytes)
     keep_launch_work = False   # diagnostics: launch_work = [(attempts per ray, latency set)] per launch
     _ctx = None
 
@@ -433,22 +482,31 @@ class RayEngine:
             return 0, 16
         return n_best, q_best
 
-    def run(self, st, p, tbound, it_begin, it_end, out, order=None, n_heavy=0, rays_per_wave=16, tails=None):
+    def run(self, st, p, tbound, it_begin, it_end, out, order=None, n_heavy=0, rays_per_wave=16, tails=None,
+            slots=None):
         """Rows ``[it_begin, it_end)`` into ``out[nray, it_end-it_begin, 8]`` (async);
-        with ``tails`` (a ``Tails``) the frozen rays' constant rows go there instead."""
+        with ``tails`` (a ``Tails``) the frozen rays' constant rows go there instead;
+        with ``slots`` (a ``Slots`` computed on ``st``) ``out`` holds the live
+        rays' row blocks only."""
         lib = H.load()
         ctx = self.ctx
         if self.bg is not None:
             ctx.set_tv_lanes(self.tv_lanes)
         if n_heavy:
             ctx.set_latency_density(rays_per_wave)
+        if slots is not None and tails is None:
+            raise ValueError("row slots need tails")
         if self.bg is None:
-            fn, bg = (lib.rwrt_rk45_run if tails is None else lib.rwrt_rk45_run_tails), H.dptr(self.packed)
+            fn, bg = (lib.rwrt_rk45_run if tails is None else lib.rwrt_rk45_run_tails if slots is None
+                      else lib.rwrt_rk45_run_slots), H.dptr(self.packed)
         else:
-            fn, bg = (lib.rwrt_rk45_run_tv if tails is None else lib.rwrt_rk45_run_tv_tails), ctypes_ref(self.bg)
+            fn, bg = (lib.rwrt_rk45_run_tv if tails is None else lib.rwrt_rk45_run_tv_tails if slots is None
+                      else lib.rwrt_rk45_run_tv_slots), ctypes_ref(self.bg)
         args = [ctx.handle, self.grid, bg, st["nray"], ctypes_ref(p), H.dptr(tbound, F64),
                 int(it_begin), int(it_end), H.dptr(order, torch.int64), int(n_heavy),
                 H.dptr(st["state"]), H.dptr(st["count"]), H.dptr(st["nanrow"]), H.dptr(out, F64)]
+        if slots is not None:
+            args += [H.dptr(slots.slot, torch.int32)]
         if tails is not None:
             args += [H.dptr(tails.frm, torch.int32), H.dptr(tails.row, F64)]
         H.check(fn(*args, H.dptr(self.work), self._stream()))
@@ -636,8 +694,19 @@ class RayEngine:
             bounds.append((i0, min(i0 + chunk, end)))
             i0 = bounds[-1][1]
         rows_max = max([b - a for a, b in bounds] or [1])
-        bufs = _row_buffers(out, nray, rows_max, self.device)
+        use_slots = (self.use_slots and self.use_tails and nray > 0
+                     and (getattr(sink, "takes_slots", False) or (sink is None and out is None)))
+        sbufs = None
+        nblk = nray   # row blocks per buffer
+        if use_slots:
+            # the first launch's live rays: the most any launch of the run has
+            first = Slots(nray, self.device).compute(st, self._stream())
+            nblk = max(1, first.count())
+        bufs = _row_buffers(out, nblk, rows_max, self.device)
+        self.rows_bytes = sum(b.numel() for b in bufs) * 8
         tbufs = [self.tails(nray) for _ in bufs]   # (alternating with the row buffers)
+        if use_slots:
+            sbufs = [first] + [Slots(nray, self.device) for _ in bufs[1:]]
         order = None
         if prev_work is None or order_policy not in ("cost", "priority", "cell", "total"):
             order = self.live_first_order_of(st)
@@ -662,7 +731,12 @@ class RayEngine:
                     print(f"split: rank correlation {rho:.3f} -> {'split' if rho < self.SPLIT_RHO else 'one launch'}",
                           flush=True)
             flat = bufs[k % len(bufs)].view(-1)
-            view = flat[: nray * (i1 - i0) * H.NOUT].view(nray, i1 - i0, H.NOUT)
+            view = flat[: nblk * (i1 - i0) * H.NOUT].view(nblk, i1 - i0, H.NOUT)
+            slots = None
+            if sbufs is not None:
+                slots = sbufs[k % len(sbufs)]
+                if k > 0:   # (the first launch's were computed above)
+                    slots.compute(st, self._stream())
             work = None
             if order_policy in ("cost", "priority", "cell", "total") and prev_work is not None:
                 # the previous launch's attempts per ray, or ("total") all of them so far
@@ -681,17 +755,17 @@ class RayEngine:
             tails = tbufs[k % len(bufs)]
             if events is not None:
                 e0, e1, es = self._event_pair()
-                self.run(st, p, tb, i0, i1, view, order, n_heavy, qpw, tails)
+                self.run(st, p, tb, i0, i1, view, order, n_heavy, qpw, tails, slots)
                 e1.record(es)
                 events.append((e0, e1))
             else:
-                self.run(st, p, tb, i0, i1, view, order, n_heavy, qpw, tails)
+                self.run(st, p, tb, i0, i1, view, order, n_heavy, qpw, tails, slots)
             if auto_split and k < n_lead:
                 works = (works + [cnt.sum(1) - prev_work])[-2:]
             if self.keep_launch_work:   # (diagnostics: each launch's attempts per ray and its latency set)
                 self.launch_work.append((cnt.sum(1) - prev_work, order[:n_heavy].clone() if n_heavy else None))
             if sink is not None:
-                deliver(self, sink, i0, i1, view, tails)
+                deliver(self, sink, i0, i1, view, tails, slots)
             elif tails is not None and out is not None:
                 self.expand(view, tails, i0, i1)   # (the caller reads its own buffer: dense rows)
             k += 1

@@ -361,11 +361,22 @@ def run_sharded(eng, y0, nt, tstep=7200.0, group=None, rank=None, world=None, pr
         prow_local, ptails_local = prow[idx], None if ptails is None else ptails.take(idx)
     last = {}
 
-    def keep(i0, i1, rows, tails=None):
+    dense = {}
+
+    def keep(i0, i1, rows, tails=None, slots=None):
         # the endpoints need each ray's last row only: a frozen ray's is its tail
-        last["row"] = rows[:, -1] if tails is None else tails.last_row(rows, i1)
+        if slots is not None:
+            last["row"] = slots.last_row(rows, tails, i1)
+        else:
+            last["row"] = rows[:, -1] if tails is None else tails.last_row(rows, i1)
         if sink is None:
             return
+        if slots is not None:
+            if getattr(sink, "takes_slots", False):
+                return sink(i0, i1, rows, idx, tails, slots)
+            # (a sink that wants dense rows: the row blocks and tails expanded)
+            dense["buf"] = slots.dense(rows, tails, i0, i1, dense.get("buf"))
+            return sink(i0, i1, dense["buf"], idx)
         if tails is not None and getattr(sink, "takes_tails", False):
             sink(i0, i1, rows, idx, tails)
         else:
@@ -373,6 +384,7 @@ def run_sharded(eng, y0, nt, tstep=7200.0, group=None, rank=None, world=None, pr
                 eng.expand(rows, tails, i0, i1)   # (a sink that wants the rows dense)
             sink(i0, i1, rows, idx)
     keep.takes_tails = True
+    keep.takes_slots = True
 
     keep(1, 1 + npr, prow_local, ptails_local)
     n_live_local = int((~frozen[idx]).sum().item())

@@ -70,6 +70,23 @@ def test_expand_tails_argument_errors():
     assert lib.rwrt_expand_tails(0, 1, 5, None, None, None, None) == H.RWRT_OK
 
 
+def test_row_slot_entry_points_validate():
+    """ABI 4 (rwrt_row_slots, rwrt_rk45_run_slots, rwrt_expand_slots)
+    validates before touching the device."""
+    lib = H.load()
+    assert lib.rwrt_row_slots(-1, None, None, None, None) == H.RWRT_ERR_ARG
+    assert lib.rwrt_row_slots(16, None, None, None, None) == H.RWRT_ERR_ARG
+    assert b"NULL" in lib.rwrt_last_error()
+    assert lib.rwrt_rk45_run_slots(None, None, None, 16, None, None, 1, 5, None, 0, None, None, None, None,
+                                   None, None, None, None, None) == H.RWRT_ERR_ARG
+    assert b"d_row_slot" in lib.rwrt_last_error()
+    assert lib.rwrt_rk45_run_tv_slots(None, None, None, 16, None, None, 1, 5, None, 0, None, None, None, None,
+                                      None, None, None, None, None) == H.RWRT_ERR_ARG
+    assert lib.rwrt_expand_slots(-1, 1, 5, None, None, None, None, None, None) == H.RWRT_ERR_ARG
+    assert lib.rwrt_expand_slots(16, 1, 5, None, None, None, None, None, None) == H.RWRT_ERR_ARG
+    assert lib.rwrt_expand_slots(0, 1, 5, None, None, None, None, None, None) == H.RWRT_OK
+
+
 def test_context_needs_a_device():
     """rwrt_ctx_create refuses a device that does not exist (none on the build
     host); destroying NULL is a no-op."""

@@ -153,3 +153,137 @@ def test_time_varying_tails_equal_dense_rows(fp32):
     y0 = torch.as_tensor(y0[:, pick].copy(), device=eng.device)
     n_start, _ = compare(run_both(eng, y0, nt, 8))
     assert n_start > 0
+
+
+# ----------------------------------------------------------------- row slots
+# ABI 4 (rwrt_rk45_run_slots): the launch's row buffer holds row blocks for
+# the rays live at its start only; rwrt_expand_slots makes them dense.
+
+class SlotRecorder:
+    """A sink that takes row blocks: keeps each launch's rows made dense
+    (rwrt_expand_slots) and its slot map, then refills the row blocks with the
+    sentinel."""
+    takes_slots = True
+
+    def __init__(self):
+        self.chunks, self.nblk = {}, set()
+
+    def __call__(self, i0, i1, view, tails, slots):
+        self.nblk.add(view.shape[0])
+        self.chunks[i0] = (i1, slots.dense(view, tails, i0, i1).clone(), slots.slot.clone())
+        view.fill_(SENTINEL)
+
+
+def run_slots(eng, y0, nt, chunk, **kw):
+    """The dense run (no tails) and the row-block run of the same rays."""
+    eng.use_tails = False
+    buf = torch.full((y0.shape[1], chunk, 8), SENTINEL, dtype=torch.float64, device=eng.device)
+    dense = Recorder(buf, False)
+    rd = eng.integrate(y0, nt, 7200.0, ttotal=(nt - 1) * 7200.0, chunk=chunk, out=buf, sink=dense, **kw)
+    eng.use_tails = True
+    rec = SlotRecorder()
+    rs = eng.integrate(y0, nt, 7200.0, ttotal=(nt - 1) * 7200.0, chunk=chunk, sink=rec, **kw)
+    assert sorted(dense.chunks) == sorted(rec.chunks)
+    for i0, (i1, dv, _) in dense.chunks.items():
+        j1, sv, _ = rec.chunks[i0]
+        assert j1 == i1
+        assert np.array_equal(bits(dv), bits(sv)), f"launch {i0}: expanded row blocks differ from the dense rows"
+    for name in ("nacc", "nrej", "nanrow"):
+        assert torch.equal(getattr(rd, name), getattr(rs, name)), name
+    assert rd.break_row == rs.break_row
+    assert np.array_equal(bits(rd.state["state"]), bits(rs.state["state"]))
+    live0 = int((~torch.isnan(y0.sum(0))).sum().item())
+    assert rec.nblk == {live0}, (rec.nblk, live0)      # one block per ray live at the start
+    return rec, eng.rows_bytes
+
+
+@pytest.mark.parametrize("n", [1, 4095, 4096, 4097, 3 * 4096 + 17, 100003])
+def test_row_slots_number_the_live_rays(n):
+    """rwrt_row_slots: the rays with a finite state mean, numbered in ray
+    order (an exclusive scan over tiles of 4 096), -1 for the others."""
+    from engine import Slots
+    rng = np.random.default_rng(n)
+    for frac in (0.0, 0.3, 0.97, 1.0):
+        s = rng.standard_normal((12, n))
+        dead = rng.random(n) < frac
+        s[rng.integers(0, 5, n)[dead], np.nonzero(dead)[0]] = np.nan
+        if n > 8:
+            s[0, 3], s[1, 3] = np.inf, -np.inf        # inf - inf: a NaN mean (frozen)
+            s[2, 5] = np.inf                          # inf: live
+            dead[3], dead[5] = True, False
+            s[:5, 5] = np.where(np.isnan(s[:5, 5]), 1.0, s[:5, 5])
+        st = dict(state=torch.as_tensor(s, device="cuda"), nray=n)
+        sl = Slots(n, torch.device("cuda")).compute(st, torch.cuda.current_stream().cuda_stream)
+        live = ~np.isnan(s[:5].sum(0) / 5.0)
+        want = np.where(live, np.cumsum(live) - 1, -1)
+        assert sl.count() == int(live.sum())
+        assert np.array_equal(sl.slot.cpu().numpy(), want), frac
+
+
+@pytest.mark.parametrize("team", [0, [64, 64, 64]])
+def test_c3_row_slots_equal_dense_rows(team):
+    """The C3 sample (16 384 live rays + 2 048 dead slots) in the bench's
+    launch shape: the row blocks, expanded, are the dense launch's rows bit for
+    bit, with and without the latency mode (quad_rays writes through its ray's
+    block too), and the buffer holds the live rays only."""
+    from bench import make_bs
+    from engine import RayEngine
+    bs, _ = make_bs("zonal")
+    eng = RayEngine.from_bs(bs)
+    y0 = c3_sample_y0(eng)
+    _, nbytes = run_slots(eng, y0, 12 * 12 + 1, 48, first_chunk=[6, 24], team=team)
+    live0 = int((~torch.isnan(y0.sum(0))).sum().item())
+    assert nbytes == live0 * 48 * 64          # one buffer of 48-row blocks (the dense one: 18 432 rays)
+
+
+@pytest.mark.parametrize("lanes,team", [(32, 0), (64, 0), (32, (64, 1))])
+def test_time_varying_row_slots_equal_dense_rows(lanes, team):
+    """The time-varying kernels (0.25 degrees, 9 six-hourly fp64 levels, 2
+    days; lane pairs, 64 rays per wave, latency waves) through row blocks."""
+    import rwrt_oracle as O
+    import synthetic as S
+    from engine import RayEngine
+    from levels import Levels
+    dt, nlev, nt = 6 * 3600.0, 9, 25
+    bl = [S.background_level(j, res=0.25) for j in range(nlev)]
+    lv = Levels(bl[0]["lat"], bl[0]["lon"], nlev, t0=0.0, dt=dt)
+    for j, b in enumerate(bl):
+        lv.set_level(j, b["u"], b["v"])
+    eng = RayEngine.from_levels(lv)
+    eng.tv_lanes = lanes
+    cfg = S.config("C5")
+    slon, slat = O.source_matrix(cfg.SW_lon, cfg.SW_lat, cfg.dlon, cfg.dlat, cfg.nnx, cfg.nny)
+    rows = eng.initial_rows(slon, slat, cfg.zwn, S.c3_freq(S.C5_PERIODS_DAYS[-1])).cpu().numpy()
+    y0 = rows[:5].reshape(5, -1)
+    pick = np.sort(np.random.default_rng(5).choice(y0.shape[1], size=8192, replace=False))
+    y0 = torch.as_tensor(y0[:, pick].copy(), device=eng.device)
+    kw = dict(order_policy="cell", first_chunk=[4], team=team) if team else {}
+    run_slots(eng, y0, nt, 8, **kw)
+
+
+def test_sharded_row_slots_equal_dense_endpoints():
+    """shard.run_sharded -- the bench's step -- with row blocks (its sink
+    takes them) against dense rows: endpoints and counters bit for bit; a
+    dense user sink behind it receives the dense rows."""
+    from bench import make_bs
+    from engine import RayEngine
+    from shard import run_sharded
+    bs, _ = make_bs("nonzonal")
+    eng = RayEngine.from_bs(bs)
+    y0 = c3_sample_y0(eng)
+    nt = 12 * 12 + 1
+    ends, rows = {}, {}
+    for slots in (False, True):
+        eng.use_slots = slots
+        got = {}
+        r = run_sharded(eng, y0, nt, 7200.0, rank=0, world=1, probe=4, lead=[24, 48], chunk=nt - 1,
+                        ttotal=(nt - 1) * 7200.0, team="auto",
+                        sink=lambda i0, i1, v, idx: got.__setitem__(i0, bits(v)))
+        ends[slots] = (bits(r.endpoints), r.counts.cpu().numpy())
+        rows[slots] = got
+    eng.use_slots = True
+    assert np.array_equal(ends[False][0], ends[True][0])
+    assert np.array_equal(ends[False][1], ends[True][1])
+    assert sorted(rows[False]) == sorted(rows[True])
+    for k in rows[False]:
+        assert np.array_equal(rows[False][k], rows[True][k]), k

@@ -105,7 +105,7 @@ def main():
         kw_w = dict(kw)
         if a.config == "C5":   # bench.py main_c5's rows per launch, capped by the row buffer's memory
             torch.cuda.empty_cache()
-            n_local = -(-int(y0.shape[1]) // w) + 2
+            n_local = -(-out["live"] // w) + 2   # (row blocks for live rays only, ABI 4)
             cap = max(1, int(0.8 * torch.cuda.mem_get_info()[0]) // (n_local * 64))
             kw_w["chunk"] = min(a.chunk or bench.c5_rows_per_launch(a.fields == "fp32", w, nt), cap)
         if w > 1 and a.shard_probe:   # every share's probe, untimed (the all-gather's result)
@@ -159,7 +159,7 @@ def main():
     kw_1 = dict(kw)
     if a.config == "C5":   # (capped by the row buffer's memory, as bench.py main_c5 caps it)
         torch.cuda.empty_cache()
-        cap = max(1, int(0.8 * torch.cuda.mem_get_info()[0]) // ((int(y0.shape[1]) + 2) * 64))
+        cap = max(1, int(0.8 * torch.cuda.mem_get_info()[0]) // ((out["live"] + 2) * 64))
         kw_1["chunk"] = min(a.chunk or bench.c5_rows_per_launch(a.fields == "fp32", 1, nt), cap)
     full = run_sharded(eng, y0, nt, rank=0, world=1, gather=False, **kw_1)
     work = (full.res.nacc + full.res.nrej)
