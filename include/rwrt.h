@@ -109,6 +109,13 @@ rwrt_status rwrt_ctx_set_latency_density(rwrt_ctx* ctx, int32_t rays_per_wave);
  * RayEngine's default, C5 fp64 1.21 -> 1.61e9 with the other round-5 changes).
  * Schedule only: results do not depend on it (ABI 3). */
 rwrt_status rwrt_ctx_set_tv_lanes(rwrt_ctx* ctx, int32_t lanes);
+/* Drain-time hand-off of this context's static-state ray loops (ABI 4): once
+ * a call's work queue is drained, a wavefront with at most max_rays rays left
+ * (0 = off, at most 16; default 16) continues them four lanes per ray, in the
+ * latency mode's layout, from exactly where they stopped (between two
+ * attempts).  Schedule only: results do not depend on it.  A call's d_work[0]
+ * counts the rays it handed off (diagnostic). */
+rwrt_status rwrt_ctx_set_handoff(rwrt_ctx* ctx, int32_t max_rays);
 /* Diagnostic ray trace of the context's rwrt_rk45_run calls (NULL / 0: off):
  * for queue positions w < capacity of the order, the ray's lane records
  * d_trace[w * 10 + 0..9] = {ray, hardware id (HW_REG_HW_ID: wave, SIMD, CU,

@@ -14,7 +14,8 @@ LIB_PATH = os.environ.get("RWRT_LIB", os.path.join(_HERE, "librwrt.so"))
 
 NFIELD_REF, NFIELD_PACK, NVAR, NMERC, NOUT, NSTATE = 18, 12, 5, 12, 8, 12
 ABI_SYMBOLS = ("rwrt_version", "rwrt_last_error", "rwrt_ctx_create", "rwrt_ctx_destroy",
-               "rwrt_ctx_set_latency_density", "rwrt_ctx_set_tv_lanes", "rwrt_ctx_set_trace",
+               "rwrt_ctx_set_latency_density", "rwrt_ctx_set_tv_lanes", "rwrt_ctx_set_handoff",
+               "rwrt_ctx_set_trace",
                "rwrt_pack_fields",
                "rwrt_mercator_point", "rwrt_rhs", "rwrt_dp54_attempt",
                "rwrt_ray_initial", "rwrt_rk45_init", "rwrt_rk45_run", "rwrt_rk45_run_tails",
@@ -99,6 +100,7 @@ def load():
         "rwrt_ctx_destroy": [_P],
         "rwrt_ctx_set_latency_density": [_P, _I32],
         "rwrt_ctx_set_tv_lanes": [_P, _I32],
+        "rwrt_ctx_set_handoff": [_P, _I32],
         "rwrt_ctx_set_trace": [_P, _P, _I64],
         "rwrt_rhs_tv": [G, B, _I64, _P, _P, _P, _P],
         "rwrt_kat_rk45": [_I32, _I64, _P, _I32, _P, _D, _D, _D, _P, _P],
@@ -176,6 +178,12 @@ class Context:
         if getattr(self, "_tvl", 64) != int(lanes):
             check(load().rwrt_ctx_set_tv_lanes(self._h, int(lanes)))
             self._tvl = int(lanes)
+
+    def set_handoff(self, max_rays):
+        """Drain-time hand-off threshold, 0..16 rays per wave (rwrt_ctx_set_handoff)."""
+        if getattr(self, "_hof", 16) != int(max_rays):
+            check(load().rwrt_ctx_set_handoff(self._h, int(max_rays)))
+            self._hof = int(max_rays)
 
     def set_trace(self, trace=None):
         """Diagnostic ray trace (rwrt_ctx_set_trace): ``trace`` an int64 device

@@ -16,6 +16,7 @@
 
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -2315,7 +2316,7 @@ struct RunArgs {
   int64_t* count;
   int32_t* nanrow;
   double* out;
-  int32_t* queue;       // [1]: the work queue's head ([0] unused)
+  int32_t* queue;       // [1]: the work queue's head; [0]: rays handed off (drain-time hand-off)
   int64_t n_heavy;      // order[0, n_heavy): rays in latency mode (quad_rays); the queue is the rest
   int32_t heavy_blocks; // blocks [0, heavy_blocks) run order[0, n_heavy) in latency mode (quad_rays)
   double cut_a;         // haversine argument certainly below cut_off (cal_dis_below)
@@ -2327,6 +2328,10 @@ struct RunArgs {
   // row_slot[j] (the rays live at the call's start, numbered in ray order by
   // rwrt_row_slots; -1 for a frozen ray, whose rows are its tail); NULL: j
   const int32_t* row_slot = nullptr;
+  // drain-time hand-off (run_rays, static state): once the queue is drained,
+  // a wave with at most this many rays left continues them in the latency
+  // mode's quad layout (0: off; rwrt_ctx_set_handoff, default 16)
+  int32_t handoff = 16;
 };
 
 // The first output row of ray `ray` in this call's row buffer (NULL when the
@@ -2677,45 +2682,17 @@ __device__ __forceinline__ bool quad_dis_reaches(const QuadRole& R, double lon_c
 // dispatch order of concurrent kernels), in the run kernel's LDS: the cell
 // cache where the run kernel keeps it, the owned stage values (20 KB) where
 // the run kernel keeps its stages.
+// quad_rays' interval loop from a ray's running state (also the drain-time
+// hand-off of rk45_run_kernel's waves, run_rays): rows [it, it_end) of `ray`,
+// its mid-step state included (in_step, rejected, hs), exactly where a run
+// kernel lane left it between two attempts
 template <bool kTrace>
-__device__ __forceinline__ void quad_rays(const RunArgs<StaticBG>& a, char* cache, double* Kq, int lb) {
-  const CachedStaticBG B = LaneBG<StaticBG>::make(a.B, cache);
-  QuadRole R;
-  R.role = threadIdx.x & 3;
-  R.odd = (R.role & 1) != 0;
-  R.high = (R.role & 2) != 0;
-  KQuad K{Kq + threadIdx.x};
-  // order position of this quad's ray, a.quad_per_wave quads per wave
-  const int qi = (threadIdx.x & 63) >> 2;
-  // consecutive positions share a wave (p -> wave p / quad_per_wave): rays of
-  // like weight, which on C3 are often near-copies whose row ends and cell
-  // crossings stay aligned.  Dealing the heaviest one per wave instead (p ->
-  // wave p % waves) mixed rays that diverge: the 256 heaviest C3 rays at 4 per
-  // wave took 14.5 us per attempt of the heaviest, 9.6 us contiguous
-  // (profiles/r4/sched/latency_xcd.txt)
-  const int64_t w = (lb * 4 + (int64_t)(threadIdx.x >> 6)) * a.quad_per_wave + qi;
-  const int64_t ray = (qi < a.quad_per_wave && w < a.n_heavy) ? a.order[w] : -1;
-  if (ray < 0) return;   // (whole quads: the four lanes share w)
-  // a ray frozen at the launch start is frozen_fill_kernel's (the C ABI asks
-  // for live rays in order[0, n_heavy); a C caller's frozen one is skipped
-  // here, not written twice)
-  if (a.frozen && a.frozen[ray]) return;
-  double y[5], f[5], aux[3];
-#pragma unroll
-  for (int v = 0; v < 5; ++v) {
-    y[v] = a.state[v * a.nray + ray];
-    f[v] = a.state[(5 + v) * a.nray + ray];
-  }
-  double t = a.state[10 * a.nray + ray], habs = a.state[11 * a.nray + ray], hs = 0.0;
-  int64_t nacc = a.count[2 * ray], nrej = a.count[2 * ray + 1];
-  const int64_t att0 = nacc + nrej;
-  double* const rows = row_block(a, ray);
-  if (kTrace && w < a.trace_cap && R.role == 0) trace_start(a.trace, w);
-  int32_t nanrow = a.nanrow[ray];
-  int32_t it = a.it_begin;
-  double prev_lon = y[0], prev_lat = y[1], cos_prev = k_cos(prev_lat);
-  aux[2] = kNaN;
-  bool in_step = false, rejected = false;
+__device__ __forceinline__ void quad_run(const RunArgs<StaticBG>& a, const CachedStaticBG& B, const QuadRole& R,
+                                         KQuad& K, int64_t ray, double* rows, double (&y)[5], double (&f)[5],
+                                         double (&aux)[3], double t, double habs, double hs, int64_t nacc,
+                                         int64_t nrej, int64_t att0, int32_t nanrow, int32_t it, double prev_lon,
+                                         double prev_lat, double cos_prev, bool in_step, bool rejected,
+                                         int64_t w) {
   const bool writer = R.role == 0;
   for (;;) {
     const double tb = a.tbound[it];
@@ -2823,6 +2800,49 @@ __device__ __forceinline__ void quad_rays(const RunArgs<StaticBG>& a, char* cach
   }
 }
 
+template <bool kTrace>
+__device__ __forceinline__ void quad_rays(const RunArgs<StaticBG>& a, char* cache, double* Kq, int lb) {
+  const CachedStaticBG B = LaneBG<StaticBG>::make(a.B, cache);
+  QuadRole R;
+  R.role = threadIdx.x & 3;
+  R.odd = (R.role & 1) != 0;
+  R.high = (R.role & 2) != 0;
+  KQuad K{Kq + threadIdx.x};
+  // order position of this quad's ray, a.quad_per_wave quads per wave
+  const int qi = (threadIdx.x & 63) >> 2;
+  // consecutive positions share a wave (p -> wave p / quad_per_wave): rays of
+  // like weight, which on C3 are often near-copies whose row ends and cell
+  // crossings stay aligned.  Dealing the heaviest one per wave instead (p ->
+  // wave p % waves) mixed rays that diverge: the 256 heaviest C3 rays at 4 per
+  // wave took 14.5 us per attempt of the heaviest, 9.6 us contiguous
+  // (profiles/r4/sched/latency_xcd.txt)
+  const int64_t w = (lb * 4 + (int64_t)(threadIdx.x >> 6)) * a.quad_per_wave + qi;
+  const int64_t ray = (qi < a.quad_per_wave && w < a.n_heavy) ? a.order[w] : -1;
+  if (ray < 0) return;   // (whole quads: the four lanes share w)
+  // a ray frozen at the launch start is frozen_fill_kernel's (the C ABI asks
+  // for live rays in order[0, n_heavy); a C caller's frozen one is skipped
+  // here, not written twice)
+  if (a.frozen && a.frozen[ray]) return;
+  double y[5], f[5], aux[3];
+#pragma unroll
+  for (int v = 0; v < 5; ++v) {
+    y[v] = a.state[v * a.nray + ray];
+    f[v] = a.state[(5 + v) * a.nray + ray];
+  }
+  double t = a.state[10 * a.nray + ray], habs = a.state[11 * a.nray + ray], hs = 0.0;
+  int64_t nacc = a.count[2 * ray], nrej = a.count[2 * ray + 1];
+  const int64_t att0 = nacc + nrej;
+  double* const rows = row_block(a, ray);
+  if (kTrace && w < a.trace_cap && R.role == 0) trace_start(a.trace, w);
+  int32_t nanrow = a.nanrow[ray];
+  int32_t it = a.it_begin;
+  double prev_lon = y[0], prev_lat = y[1], cos_prev = k_cos(prev_lat);
+  aux[2] = kNaN;
+  bool in_step = false, rejected = false;
+  quad_run<kTrace>(a, B, R, K, ray, rows, y, f, aux, t, habs, hs, nacc, nrej, att0, nanrow, it, prev_lon,
+                   prev_lat, cos_prev, in_step, rejected, w);
+}
+
 // WR.core_ray_run_rk45 (wr.py:767-887) for rows [it_begin, it_end): persistent
 // lanes, one ray each, refilled from the work queue.
 //
@@ -2864,6 +2884,9 @@ __device__ __forceinline__ void run_rays(const RunArgs<BG>& a, const LBG& lbg, c
   double* rows = nullptr;   // the ray's row block (row_block)
   int32_t it = 0, nanrow = 0, wpos = 0;   // (wpos: the ray's queue position, kTrace only)
   double prev_lon = 0.0, prev_lat = 0.0, cos_prev = 0.0;
+  // drain-time hand-off (the static state's ray loop): see below the loop
+  constexpr bool kHandoff = std::is_same<LBG, CachedStaticBG>::value && !kReplica && !kPair && !kTrace;
+  bool handoff = false;
   // above frozen_fill_kernel's waves (priority 0) sharing the SIMD: the
   // fill takes the issue cycles the ray loop leaves idle
   __builtin_amdgcn_s_setprio(1);
@@ -2910,6 +2933,17 @@ __device__ __forceinline__ void run_rays(const RunArgs<BG>& a, const LBG& lbg, c
       prev_lat = L.y[1];
       cos_prev = k_cos(prev_lat);
       L.aux[2] = kNaN;     // no evaluation at y yet
+    }
+    if constexpr (kHandoff) {
+      // (wave-uniform) few rays left in this wave and none left in the queue:
+      // hand them to the quad layout, between two attempts
+      if (RARE(__builtin_popcountll(__builtin_amdgcn_ballot_w64(true)) <= (unsigned)a.handoff)) {
+        const int32_t q = __atomic_load_n(&a.queue[1], __ATOMIC_RELAXED);
+        if (a.n_heavy + (int64_t)q >= a.nray) {
+          handoff = true;
+          break;
+        }
+      }
     }
     const double tb = a.tbound[it];
     const int st = L.iterate(P, tb, a.min_step, a.rtol, a.atol, nacc, nrej);
@@ -2994,6 +3028,56 @@ __device__ __forceinline__ void run_rays(const RunArgs<BG>& a, const LBG& lbg, c
       ray = -1;
     }
     if ((kReplica || kPair) && it == a.it_end) ray = -1;   // (the other lanes of a latency wave or pair)
+  }
+  if constexpr (kHandoff) {
+    // Drain-time hand-off.  The queue order is a prediction (the previous
+    // launch's work): the rays that end a launch run nearly alone, one lane
+    // of a wave each, for tens of ms (non-zonal C3: 3-14 rays for ~60 ms,
+    // DESIGN.md §6).  Once the queue is drained, a wave with at most
+    // a.handoff rays left moves them -- between two attempts, every register
+    // of a ray's state by ds_bpermute -- to the quad layout of the latency
+    // mode (quad_run: four lanes per ray, the divisions, stage sums and error
+    // quotients dealt out over the quad; 1.26-1.37x per attempt, DESIGN.md
+    // §4) and continues each from exactly where its lane stopped: the same
+    // operations on the same values, so the rows and counters are the run
+    // kernel's bit for bit.  The lanes that left the loop with no ray join in.
+    const uint64_t hm = __builtin_amdgcn_ballot_w64(handoff);
+    if (RARE(hm != 0)) {
+      const int q = (int)((threadIdx.x & 63u) >> 2);
+      const int nq = __builtin_popcountll(hm);
+      uint64_t m = hm;
+      for (int i = 0; i < q && m; ++i) m &= m - 1;   // the q-th ray's lane
+      const int src = m ? __builtin_ctzll(m) : 0;
+      auto sh = [&](double v) { return __shfl(v, src); };
+      auto shl = [&](int64_t v) { return (int64_t)__shfl((long long)v, src); };
+      auto shi = [&](int32_t v) { return (int32_t)__shfl((int)v, src); };
+      double y[5], f[5], aux[3];
+#pragma unroll
+      for (int v = 0; v < 5; ++v) {
+        y[v] = sh(L.y[v]);
+        f[v] = sh(L.f[v]);
+      }
+#pragma unroll
+      for (int v = 0; v < 3; ++v) aux[v] = sh(L.aux[v]);
+      const int64_t qray = shl(ray), qnacc = shl(nacc), qnrej = shl(nrej);
+      double* const qrows = reinterpret_cast<double*>(shl(reinterpret_cast<int64_t>(rows)));
+      const double qt = sh(L.t), qhabs = sh(L.habs), qhs = sh(L.hs);
+      const double qplon = sh(prev_lon), qplat = sh(prev_lat), qcos = sh(cos_prev);
+      const int32_t qnanrow = shi(nanrow), qit = shi(it);
+      const int32_t qflags = shi((L.in_step ? 1 : 0) | (L.rejected ? 2 : 0));
+      if ((threadIdx.x & 63u) == 0) atomicAdd(&a.queue[0], nq);   // (rays handed off: d_work[0])
+      if (q < nq) {   // (whole quads)
+        CachedStaticBG QB = lbg;
+        QB.key_x = QB.key_y = ~0u;   // the quad refill fills other slots of the slice
+        QuadRole R;
+        R.role = threadIdx.x & 3;
+        R.odd = (R.role & 1) != 0;
+        R.high = (R.role & 2) != 0;
+        KQuad K{reinterpret_cast<double*>(smem) + threadIdx.x};
+        quad_run<false>(a, QB, R, K, qray, qrows, y, f, aux, qt, qhabs, qhs, qnacc, qnrej, 0, qnanrow, qit,
+                        qplon, qplat, qcos, (qflags & 1) != 0, (qflags & 2) != 0, 0);
+      }
+    }
   }
 }
 
@@ -3625,6 +3709,7 @@ struct rwrt_ctx {
   hipEvent_t done = nullptr;   // end of the last call on this context
   int quad_per_wave = 16;      // latency mode: rays per wave (rwrt_ctx_set_latency_density)
   int tv_lanes = 64;           // rays per wave of fp64 time-varying calls (rwrt_ctx_set_tv_lanes)
+  int handoff = 16;            // drain-time hand-off threshold (rwrt_ctx_set_handoff)
   int64_t* trace = nullptr;    // rwrt_ctx_set_trace (diagnostic)
   int64_t trace_cap = 0;
   bool used = false;
@@ -3760,6 +3845,7 @@ rwrt_status launch_run(rwrt_ctx* ctx, const BG& B, int64_t nray, const rwrt_para
   // latency-mode grid and launching it
   std::lock_guard<std::mutex> lock(ctx->mu);
   const int32_t quad_per_wave = ctx->quad_per_wave;
+  const int32_t handoff = ctx->handoff;
   // rays per latency-mode block: quad_rays 4 x rays-per-wave, the
   // time-varying latency waves one ray per wave
   const int64_t per_block = BG::kTimeVarying ? 4 : 4 * (int64_t)quad_per_wave;
@@ -3783,6 +3869,7 @@ rwrt_status launch_run(rwrt_ctx* ctx, const BG& B, int64_t nray, const rwrt_para
                 d_tbound, d_order, d_state, d_count, d_nanrow, d_out, d_work,
                 n_heavy, 0, haversine_cut(p->cut_off), nullptr};
   a.row_slot = d_row_slot;
+  a.handoff = handoff;
   // frozen rays: flagged on `stream`, filled on the context's side stream
   // while the run kernel (which skips them) integrates the rest; `stream` then
   // waits for the fill, so the call stays one stream-ordered operation.  With
@@ -4143,6 +4230,14 @@ rwrt_status rwrt_ctx_set_tv_lanes(rwrt_ctx* c, int32_t lanes) {
   if (lanes != 32 && lanes != 64) return fail(RWRT_ERR_ARG, "time-varying lanes per wave must be 32 or 64%s");
   std::lock_guard<std::mutex> lock(c->mu);
   c->tv_lanes = lanes;
+  return RWRT_OK;
+}
+
+rwrt_status rwrt_ctx_set_handoff(rwrt_ctx* ctx, int32_t max_rays) {
+  if (rwrt_status s = ctx_check(ctx)) return s;
+  if (max_rays < 0 || max_rays > 16) return fail(RWRT_ERR_ARG, "hand-off threshold must be 0..16 rays%s");
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  ctx->handoff = max_rays;
   return RWRT_OK;
 }
 

@@ -142,6 +142,10 @@ class RayEngine:
     # one, gets a row buffer of live rays x rows instead of every slot x rows
     # (C3: 49.5 GB instead of 166 GB); other sinks get dense rows as before
     use_slots = os.environ.get("RWRT_SLOTS", "1") != "0"
+    # drain-time hand-off of the static ray loop (rwrt_ctx_set_handoff): a wave
+    # with at most this many rays left once the queue is drained continues
+    # them in the quad layout (0: off).  Schedule only.
+    handoff = int(os.environ.get("RWRT_HANDOFF", "16"))
 
     def __init__(self, fields, lon, lat, device=None):
         """``fields``: the reference stack ``[nlon(+1), nlat, 18]`` (numpy or tensor);
@@ -164,6 +168,12 @@ class RayEngine:
     split_rho = None   # the last advance()'s rank correlation of its leading launches (split="auto")
     launch_log = ()    # the last advance()'s launches: rows and latency-mode decision
     rows_bytes = 0     # the last advance()'s row buffers (device bytes)
+    launch_handoffs = ()   # the last advance()'s rays handed off per launch (device; handoffs())
+
+    def handoffs(self):
+        """Rays the drain-time hand-off moved to the quad layout, per launch of
+        the last ``advance`` (waits for them)."""
+        return [int(h.item()) for h in self.launch_handoffs]
     keep_launch_work = False   # diagnostics: launch_work = [(attempts per ray, latency set)] per launch
     _ctx = None
 
@@ -494,6 +504,7 @@ class RayEngine:
             ctx.set_tv_lanes(self.tv_lanes)
         if n_heavy:
             ctx.set_latency_density(rays_per_wave)
+        ctx.set_handoff(self.handoff)
         if slots is not None and tails is None:
             raise ValueError("row slots need tails")
         if self.bg is None:
@@ -714,6 +725,7 @@ class RayEngine:
         self.split_rho = None
         auto_split, split_rows = self.parse_split(split)   # (cuts of the long launch)
         self.launch_log = []   # per launch: rows, rays in latency mode (diagnostics)
+        self.launch_handoffs = []   # per launch: rays handed off at the drain (device int32)
         self.launch_work = []
         k = 0
         while k < len(bounds):
@@ -760,6 +772,7 @@ class RayEngine:
                 events.append((e0, e1))
             else:
                 self.run(st, p, tb, i0, i1, view, order, n_heavy, qpw, tails, slots)
+            self.launch_handoffs.append(self.work[0:1].clone())   # (rays handed off, rwrt_ctx_set_handoff)
             if auto_split and k < n_lead:
                 works = (works + [cnt.sum(1) - prev_work])[-2:]
             if self.keep_launch_work:   # (diagnostics: each launch's attempts per ray and its latency set)

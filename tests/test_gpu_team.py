@@ -77,3 +77,40 @@ def test_team_equals_run_kernel_c2(kind):
         assert same(got[:, :, :7], want[:, :, :7]), team
         assert torch.equal(rg.nacc, rw.nacc) and torch.equal(rg.nrej, rw.nrej), team
         assert torch.equal(rg.nanrow, rw.nanrow), team
+
+
+@pytest.mark.parametrize("kind", ["zonal", "nonzonal"])
+def test_drain_handoff_equals_run_kernel(kind):
+    """The drain-time hand-off (rwrt_ctx_set_handoff): once a launch's queue is
+    drained, a wave with at most N rays left continues them in the quad layout
+    from where each lane stopped, mid-step state included.  C2 (3 072 slots,
+    10 days, chunked) and the C3 sample (12 days, the bench's launch shape) at
+    N = 16, 4 and 1 against the hand-off off: rows, accepted / rejected counts
+    and early-exit rows bit for bit, and rays were handed off."""
+    from bench import c3_initial_state, make_bs
+    from engine import RayEngine
+    from wr import initial_rows
+    bs, _ = make_bs(kind)
+    eng = RayEngine.from_bs(bs)
+    cfg = S.config("C2")
+    ix, iy = np.meshgrid(np.arange(cfg.nnx), np.arange(cfg.nny))
+    lon = ((cfg.SW_lon % 360.0 + ix.ravel() * cfg.dlon) % 360.0) * np.pi / 180.0
+    lat = (cfg.SW_lat + iy.ravel() * cfg.dlat) * np.pi / 180.0
+    with np.errstate(all="ignore"):
+        c2 = np.array(initial_rows(bs, lon, lat, cfg.zwn, cfg.freq)[:5]).reshape(5, -1)
+    c3 = c3_initial_state(bs)[:, golden("c3_sample.npz")["idx"]]
+    for y0, nt, kw in ((c2, 10 * 12 + 1, dict(chunk=40, first_chunk=[7])),
+                       (c3, 12 * 12 + 1, dict(chunk=48, first_chunk=[6, 24], team=[64, 64, 64]))):
+        eng.handoff = 0
+        want, rw = rows_of(eng, y0, nt, **kw)
+        assert sum(eng.handoffs()) == 0
+        for n in (16, 4, 1):
+            eng.handoff = n
+            got, rg = rows_of(eng, y0, nt, **kw)
+            moved = eng.handoffs()
+            assert sum(moved) > 0, (n, moved)
+            assert same(got[:, :, :7], want[:, :, :7]), n
+            assert same(got[:, :, 7], want[:, :, 7]), n
+            assert torch.equal(rg.nacc, rw.nacc) and torch.equal(rg.nrej, rw.nrej), n
+            assert torch.equal(rg.nanrow, rw.nanrow), n
+    eng.handoff = 16
