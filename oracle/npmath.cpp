@@ -73,6 +73,13 @@ void nm_sincostan_split_arr(const double* x, double* s, double* c, double* t, in
     nm_sincostan_end(x[i], p, s[i], c[i], t[i]);
   }
 }
+// sin (want_cos[i] == 0) or cos of x[i] through the team form (nm_sinorcostan_*)
+void nm_sinorcos_arr(const double* x, const int32_t* want_cos, double* out, double* tn, int64_t n) {
+  for (int64_t i = 0; i < n; ++i) {
+    const SinOrCosTanPre p = nm_sinorcostan_begin(x[i], want_cos[i] != 0);
+    nm_sinorcostan_end(x[i], want_cos[i] != 0, p, out[i], tn[i]);
+  }
+}
 void nm_rcp14_arr(const double* x, double* out, int64_t n) {
   for (int64_t i = 0; i < n; ++i) out[i] = nm_rcp14(x[i]);
 }

@@ -438,6 +438,84 @@ NM_FN void nm_sincostan_end(double x, const SinCosTanPre& r, double& sn, double&
   }
 }
 
+// sin OR cos of one argument per lane, one instruction stream for both (the
+// lanes of a ray team, csrc/rwrt.hip: lane pairs of the fp64 time-varying loop,
+// quads of the latency mode): nm_sincos_fin evaluates one do_sin and one
+// do_cos per lane; a lane that wants only sin(x) or only cos(x) needs one of
+// them -- do_sin(x, 0) / do_cos(x, 0) below 0.855469, do_cos(t, pi/2 tail) /
+// do_sin(a, da) above -- and do_sin_t and do_cos_t are the same operations on
+// permuted operands: the table pair (sn, ssn, cs, ccs) read as (cs, ccs, sn,
+// ssn), s negated, the tail added to xr or folded into s, the correction
+// term's product dropped.  So a sin lane and a cos lane run one stream,
+// selecting operands, and read ONE table point each.  Bit for bit nm_sin(x)
+// / nm_cos(x) for |x| < 2.426265 (tests/test_np_math.py; the rest: the
+// caller's rare branch, nm_sinorcostan_end).
+NM_FN unsigned nm_sinorcos_index(double x, bool want_cos) {
+  const bool far = g_hi(x) >= 0x3FEB6000u;
+  const double t = nm_d(kG_HP0) - nm_abs(x);
+  const double a = t + nm_d(kG_HP1);
+  return g_index(far ? ((want_cos != far) ? t : a) : x);
+}
+NM_FN double nm_sinorcos_fin(double x, bool want_cos, const GTab& T) {
+  const unsigned k = g_hi(x);
+  const bool far = k >= 0x3FEB6000u;
+  const double t = nm_d(kG_HP0) - nm_abs(x);
+  const double a = t + nm_d(kG_HP1);
+  const double da = (t - a) + nm_d(kG_HP1);
+  const bool ev_cos = want_cos != far;                         // this lane's evaluation is do_cos
+  const double u = far ? (ev_cos ? t : a) : x;
+  const double du = far ? (ev_cos ? nm_d(kG_HP1) : da) : 0.0;
+  const double ts = g_taylor_sin(u, du);                       // (do_sin, |u| < 0.126)
+  const double dxs = ev_cos ? ((u < 0.0) ? -du : du) : ((0.0 < u) ? du : -du);
+  const double au = nm_abs(u);
+  const double uu = nm_d(kG_BIG) + au;
+  const double r0 = au - (uu - nm_d(kG_BIG));
+  const double xr = ev_cos ? r0 + dxs : r0;
+  const double xx = xr * xr;
+  const double tt = nm_fma(nm_d(kG_SN5), xx, nm_d(kG_SN3));
+  const double q = nm_fma(xr * xx, tt, ev_cos ? xr : dxs);
+  const double s = ev_cos ? q : xr + q;
+  double c0 = nm_fma(nm_d(kG_CS6), xx, nm_d(kG_CS4));
+  c0 = nm_fma(c0, xx, nm_d(kG_CS2));
+  const double m = xx * c0;
+  const double c = ev_cos ? m : nm_fma(xr, dxs, m);
+  const double P = ev_cos ? T.cs : T.sn, p = ev_cos ? T.ccs : T.ssn;
+  const double Q = ev_cos ? T.sn : T.cs, qq = ev_cos ? T.ssn : T.ccs;
+  const double s2 = ev_cos ? -s : s;
+  const double cor = nm_fma(s2, Q, nm_fma(-c, P, nm_fma(qq, s2, p)));
+  const double r = P + cor;
+  double v = ev_cos ? r : (nm_abs(u) < nm_d(kG_T126) ? ts : nm_copysign(r, u));
+  v = (!want_cos && far) ? nm_copysign(v, x) : v;
+  return want_cos ? ((k < 0x3E400000u) ? 1.0 : v) : ((k < 0x3E500000u) ? x : v);
+}
+// (sin or cos) and tan of one argument in two halves, as nm_sincostan_begin /
+// _end: one table point for the trigonometric pair instead of two
+struct SinOrCosTanPre {
+  GTab T;
+  TanPre tp;
+  unsigned A, Nk;
+};
+NM_FN SinOrCosTanPre nm_sinorcostan_begin(double x, bool want_cos) {
+  SinOrCosTanPre r;
+  const int j = t_index(x);
+  double T, Tl;
+  NM_TAN2(j, T, Tl);
+  r.T = g_tab(nm_sinorcos_index(x, want_cos));
+  NM_ISSUE_FENCE();
+  r.tp = nm_tan_pre(x, T, Tl);
+  const unsigned k = rcp14_knot(r.tp.D);
+  NM_KNOT2(k, r.A, r.Nk);
+  return r;
+}
+NM_FN void nm_sinorcostan_end(double x, bool want_cos, const SinOrCosTanPre& r, double& sc, double& tn) {
+  sc = nm_sinorcos_fin(x, want_cos, r.T);
+  tn = nm_tan_fin(r.tp, r.A, r.Nk);
+  if (NM_RARE(nm_sincos_rare(x))) {                                    // |x| >= 2.426265, inf, NaN (rare)
+    sc = want_cos ? nm_cos(x) : nm_sin(x);
+    tn = nm_tan(x);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // SVML __svml_pow8_ha (main path): log2 x = k + log2 of the table point + a
 // degree-10 polynomial in r = (m R - 1) / 2 (R = VRCP14 of the mantissa,

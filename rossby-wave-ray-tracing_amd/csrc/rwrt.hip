@@ -1649,6 +1649,44 @@ __device__ __forceinline__ void ray_rhs(const BG& B, double t, const double* y, 
   }
 }
 
+// ray_rhs for a lane pair (PairVaryingBG64: lanes L and L + 32 hold one ray):
+// the lower lane evaluates sin(lat), the upper one cos(lat) -- one do_sin /
+// do_cos stream and one table point per lane (np_math.h nm_sinorcos_fin) --
+// exchanged by v_permlane32_swap; everything else as ray_rhs.
+#ifndef RWRT_TEAM_SINORCOS
+#define RWRT_TEAM_SINORCOS 1
+#endif
+#if RWRT_TEAM_SINORCOS
+__device__ __forceinline__ void ray_rhs(const PairVaryingBG64& B, double t, const double* y, double* dy,
+                                        double* aux = nullptr) {
+  const double lon = y[0], lat = y[1], kx = y[2];
+  const bool bad = fabs(lat) >= kHalfPi || fabs(y[3]) >= 100.0;
+  const double ky = bad ? kNaN : y[3], amp = y[4];
+  double g[11];
+  const auto trig = np_math::nm_sinorcostan_begin(lat, B.upper);
+  DivGuard G;
+  KapTermsR kw;
+  const auto pending = lookup_begin(B, lon, lat, t);
+  double sc, tn;
+  np_math::nm_sinorcostan_end(lat, B.upper, trig, sc, tn);
+  double s, c;
+  PairVaryingBG64::both(sc, s, c);
+  __builtin_amdgcn_sched_barrier(0);
+  lookup_end(B, pending, g, [&] { kw = kap_terms_r(kx, ky, G); });
+  const Merc M = merc_factors(lat, c, s);
+  double ug, vg;
+  if (RARE(!rhs_tail_fast(g, M, s, c, tn, kx, kw, G, amp, dy, ug, vg))) {
+    asm volatile("");   // an operand outside qdiv's exact range, or the pole band (rare branch)
+    rhs_tail_ieee(g, M, s, c, tn, kx, ky, amp, dy, ug, vg);
+  }
+  if (aux) {
+    aux[0] = ug;
+    aux[1] = vg;
+    aux[2] = bad ? kNaN : c;
+  }
+}
+#endif
+
 // ray_rhs with fp32 arithmetic on fp32 levels (VaryingBGA32): the same
 // expressions as ray_rhs / mercator12 / ugvg / core_diffun in float, the
 // device library's sinf/cosf/tanf; dy and aux are returned in fp64.
@@ -2478,15 +2516,27 @@ __device__ __forceinline__ void quad_rhs(const CachedStaticBG& B, const QuadRole
   const bool bad = fabs(lat) >= kHalfPi || fabs(y[3]) >= 100.0;
   const double ky = bad ? kNaN : y[3], amp = y[4];
   double g[11];
+  // sin on roles 0 and 2, cos on roles 1 and 3: one do_sin / do_cos stream
+  // and one table point per lane (np_math.h nm_sinorcos_fin), then broadcast
+#if RWRT_TEAM_SINORCOS
+  const auto trig = np_math::nm_sinorcostan_begin(lat, R.odd);
+#else
   const auto trig = np_math::nm_sincostan_begin(lat);
+#endif
   MARK("trig_begin_done");
   const KapTerms kw = kap_terms(kx, ky);
   MARK("kap_done");
   const int rb = R.high ? R.role : R.role + 4;
   const auto pending = B.quad_begin(lon, lat, (unsigned)R.role * 1024u, (unsigned)(rb - 1) * 1024u);
   MARK("cell_done");
+#if RWRT_TEAM_SINORCOS
+  double sc, tn;
+  np_math::nm_sinorcostan_end(lat, R.odd, trig, sc, tn);
+  const double s = qbcast<0>(sc), c = qbcast<1>(sc);
+#else
   double s, c, tn;
   np_math::nm_sincostan_end(lat, trig, s, c, tn);
+#endif
   MARK("trig_end_done");
   __builtin_amdgcn_sched_barrier(0);
   quad_lookup_end(B, R, pending, g);

@@ -180,3 +180,22 @@ def test_rcp14_restatement(lib):
     p2 = 2.0 ** np.arange(-1000, 1000, 7, dtype=np.float64)
     assert np.array_equal(unary(lib, "nm_rcp14_arr", p2), 1.0 / p2)
     assert np.array_equal(unary(lib, "nm_rcp14_arr", -x), -r)
+
+
+def test_team_sin_or_cos_is_sin_and_cos(lib):
+    """nm_sinorcostan_begin/_end (the ray teams' trigonometry: a lane pair or a
+    quad shares a ray, each lane evaluates sin OR cos in one instruction
+    stream from one table point) == NumPy's sin and cos bit for bit, with the
+    same tan, on every argument class of the other tests."""
+    lib.nm_sinorcos_arr.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_int64]
+    x = trig_args(np.random.default_rng(11), 1 << 23)
+    x = x[~(np.abs(x) > 65536.0)]
+    with np.errstate(all="ignore"):
+        want = {0: np.sin(x), 1: np.cos(x)}
+    want_tan = unary(lib, "nm_tan_arr", x)
+    for flag in (0, 1):
+        f = np.full(x.size, flag, np.int32)
+        out, tn = np.empty_like(x), np.empty_like(x)
+        lib.nm_sinorcos_arr(x.ctypes.data, f.ctypes.data, out.ctypes.data, tn.ctypes.data, x.size)
+        assert_bitwise(out, want[flag], x, "cos" if flag else "sin")
+        assert_bitwise(tn, want_tan, x, "tan")
