@@ -1653,38 +1653,12 @@ __device__ __forceinline__ void ray_rhs(const BG& B, double t, const double* y, 
 // the lower lane evaluates sin(lat), the upper one cos(lat) -- one do_sin /
 // do_cos stream and one table point per lane (np_math.h nm_sinorcos_fin) --
 // exchanged by v_permlane32_swap; everything else as ray_rhs.
+// (A lane pair could evaluate sin on its lower lane and cos on its upper one
+// (np_math.h nm_sinorcos_fin, as quad_rhs does): 1.2 % slower on C5 fp64,
+// profiles/r6/sinorcos_ab.txt -- the operand selects cost what the second
+// evaluation did, and the exchange adds its latency to the serial chain.)
 #ifndef RWRT_TEAM_SINORCOS
 #define RWRT_TEAM_SINORCOS 1
-#endif
-#if RWRT_TEAM_SINORCOS
-__device__ __forceinline__ void ray_rhs(const PairVaryingBG64& B, double t, const double* y, double* dy,
-                                        double* aux = nullptr) {
-  const double lon = y[0], lat = y[1], kx = y[2];
-  const bool bad = fabs(lat) >= kHalfPi || fabs(y[3]) >= 100.0;
-  const double ky = bad ? kNaN : y[3], amp = y[4];
-  double g[11];
-  const auto trig = np_math::nm_sinorcostan_begin(lat, B.upper);
-  DivGuard G;
-  KapTermsR kw;
-  const auto pending = lookup_begin(B, lon, lat, t);
-  double sc, tn;
-  np_math::nm_sinorcostan_end(lat, B.upper, trig, sc, tn);
-  double s, c;
-  PairVaryingBG64::both(sc, s, c);
-  __builtin_amdgcn_sched_barrier(0);
-  lookup_end(B, pending, g, [&] { kw = kap_terms_r(kx, ky, G); });
-  const Merc M = merc_factors(lat, c, s);
-  double ug, vg;
-  if (RARE(!rhs_tail_fast(g, M, s, c, tn, kx, kw, G, amp, dy, ug, vg))) {
-    asm volatile("");   // an operand outside qdiv's exact range, or the pole band (rare branch)
-    rhs_tail_ieee(g, M, s, c, tn, kx, ky, amp, dy, ug, vg);
-  }
-  if (aux) {
-    aux[0] = ug;
-    aux[1] = vg;
-    aux[2] = bad ? kNaN : c;
-  }
-}
 #endif
 
 // ray_rhs with fp32 arithmetic on fp32 levels (VaryingBGA32): the same
