@@ -255,8 +255,11 @@ def schedule_defaults(args, world):
     """The schedule knobs left unset on the command line, by what one GPU
     holds: a whole C3 set (one GPU, or weak scaling) or a split one / C5.
       first launches  24 + 160 rows (a whole set: throughput-bound, a longer
-                      second re-ordering launch orders the last one better),
-                      24 + 96 otherwise (profiles/r2/ab/launch_sweep.txt);
+                      second re-ordering launch orders the last one better,
+                      profiles/r2/ab/launch_sweep.txt); a split C3 set 96
+                      (chain-bound ranks: one re-ordering launch fewer, 8
+                      ranks 0.196 s against 0.201 with 24 + 96, 24 alone
+                      0.259 -- profiles/r6/c4_lead_sweep.txt); C5 24 + 96;
       probe           4 rows for a whole C3 set (+0.75 % over 6 with the
                       per-launch latency mode, profiles/r3/sched/pass_w_*),
                       6 otherwise;
@@ -271,7 +274,7 @@ def schedule_defaults(args, world):
                       pass_x_*); a split set: the auto rule (RayEngine.team_size)."""
     whole = args.config == "C3" and (world == 1 or args.scaling == "weak")
     if args.first_chunk is None:
-        args.first_chunk = "24,160" if whole else "24,96"
+        args.first_chunk = "24,160" if whole else ("96" if args.config == "C3" else "24,96")
     if args.probe is None:
         args.probe = 4 if whole else 6
     if args.team is None:

@@ -108,7 +108,7 @@ def test_schedule_defaults():
     a = bench.schedule_defaults(ns(bg="nonzonal"), 8)
     assert (a.first_chunk, a.probe, a.team) == ("24,160", 4, "0")
     a = bench.schedule_defaults(ns(scaling="strong"), 8)
-    assert (a.first_chunk, a.probe, a.team) == ("24,96", 6, "auto")
+    assert (a.first_chunk, a.probe, a.team) == ("96", 6, "auto")
     a = bench.schedule_defaults(ns(scaling="strong"), 1)
     assert (a.first_chunk, a.probe, a.team) == ("24,160", 4, "64,64,64")
     # C5: no latency mode by default (its launch-ending rays are not predictable)
