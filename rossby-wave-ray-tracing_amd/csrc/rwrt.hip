@@ -1050,11 +1050,15 @@ struct PairVaryingBG64 {
       if (2 * q + 1 < 11) go[2 * q + 1] = VaryingBG<double>::bl(p.w, v[0][q].y, v[1][q].y, v[2][q].y, v[3][q].y);
     }
     MARK("p_blend");
+    // g = g_A (1 - w) + g_B w: each lane forms its own level's product, the
+    // swap hands both products to every lane, one add -- the same operations
+    // on the same operands (4 instructions per field instead of 5)
+    const double f = upper ? p.wt : 1.0 - p.wt;
 #pragma unroll
     for (int i = 0; i < 11; ++i) {
-      double ga, gb;
-      both(go[i], ga, gb);
-      g[i] = ga * (1.0 - p.wt) + gb * p.wt;
+      double pa, pb;
+      both(go[i] * f, pa, pb);
+      g[i] = pa + pb;
     }
   }
   __device__ __forceinline__ void interp4(double lon, double lat, double t, double& fu, double& fv,
@@ -1605,6 +1609,41 @@ __device__ __forceinline__ bool rhs_tail_fast(const double g[11], const Merc& M,
   return G.ok() & (M.m == 1.0);
 }
 
+// rhs_tail_fast for a lane pair's split outputs: the same operations, but
+// each lane divides only the numerators of its own variables by R -- the
+// lower lane dy0, dy2, the upper one dy1, dy3 (the same operation shape on
+// the other operand), both dy4 -- returned as (dA, dB, dC) (pair_attempt)
+__device__ __forceinline__ bool rhs_tail_fast_pair(const double g[11], const Merc& M, double s, double c,
+                                                   double tn, double kx, const KapTermsR& kw, DivGuard G,
+                                                   double amp, bool up, double& dA, double& dB, double& dC,
+                                                   double& ug, double& vg) {
+  const double fu = g[F_U], fv = g[F_V];
+  const double rc = rcp2(c);
+  const double fmu = qdiv(fu, c, rc, G), fmv = qdiv(fv, c, rc, G);
+  const double fmux = qdiv(g[F_UX], c, rc, G), fmvx = qdiv(g[F_VX], c, rc, G);
+  const double fmuy = g[F_UY] + tn * fu, fmvy = g[F_VY] + tn * fv;
+  const double fmqx = g[F_QX], fmqy = g[F_QY] * c, fmqxx = g[F_QXX];
+  const double fmqyx = g[F_QXY] * c, fmqxy = fmqyx;
+  const double fmqyy = ((g[F_QYY] * c) - (g[F_QY] * s)) * c;
+  const double kap = kw.kap, kap2 = kw.kap2;
+  ug = fmu + qdiv(((1.0 - kap2) * fmqy) - ((2.0 * kap) * fmqx), kw.denom, kw.rden, G);
+  vg = fmv + qdiv(((2.0 * kap) * fmqy) + ((1.0 - kap2) * fmqx), kw.denom, kw.rden, G);
+  const double qk = qdiv(kap * fmqxx - fmqyx, kw.kk, kw.rkk, G);
+  const double ql = qdiv(kap * fmqxy - fmqyy, kw.kk, kw.rkk, G);
+  const double dzwn = (-kx) * ((fmux + kap * fmvx) + qk);
+  const double dmwn = (-kx) * ((fmuy + kap * fmvy) + ql);
+  const double damp1 = qdiv(2.0 * ((fmux + fmvy) + kap * (fmvx + fmuy)), kw.kap1, kw.rk1, G);
+  const double damp2 = qdiv(2.0 * (kap * (fmqxx - fmqyy) + (kap2 - 1.0) * fmqxy), kw.denom, kw.rden, G);
+  const double damp3 = (-2.0 * s) * fmv;
+  const double damp = (damp1 + damp2) + damp3;
+  const double rR = rcp2(kREarth);   // (loop-invariant)
+  const double vgc = vg * c;
+  dA = qdiv(up ? vgc : ug, kREarth, rR, G);
+  dB = qdiv(up ? dmwn : dzwn, kREarth, rR, G);
+  dC = qdiv(damp * amp, kREarth, rR, G);
+  return G.ok() & (M.m == 1.0);
+}
+
 // aux (optional) receives {ug, vg, cos(lat)} of this evaluation -- exactly what
 // the per-interval post-processing recomputes at the same position
 // (wr.py:844, 856-865) -- or NaN for a masked ray (no values computed).
@@ -2094,6 +2133,145 @@ __device__ __forceinline__ double dp54_attempt(const P& fun, KS& K, double t, co
   return sqrt(ss) / RootN<NV>::v;
 }
 
+// ---------------------------------------------------------------------------
+// Lane pairs (fp64 time-varying loop, PairVaryingBG64): lanes L and L + 32
+// hold one ray.  Besides the two levels' blends (PairVaryingBG64::end), the
+// work that is the same operation on other operands is dealt out over the
+// pair instead of done twice: the lower lane owns variables 0 and 2, the
+// upper one 1 and 3, both 4 -- the RHS's final divisions by R (dy0 = ug / R
+// | dy1 = vg cos / R, dy2 = dzwn / R | dy3 = dmwn / R), the stage sums and
+// stage values K1..K5 (three per lane in LDS instead of five), the error
+// estimate's quotients -- and exchanged by v_permlane32_swap (both()).  Every
+// value is the same operation on the same operands as in ray_rhs /
+// dp54_attempt: results are bit for bit the 64-lane loop's.
+// ---------------------------------------------------------------------------
+// ray_rhs for a pair: (dA, dB, dC) = this lane's (dy0 | dy1, dy2 | dy3, dy4)
+__device__ __forceinline__ void pair_rhs(const PairVaryingBG64& B, double t, const double* y, double& dA,
+                                         double& dB, double& dC, double* aux) {
+  const double lon = y[0], lat = y[1], kx = y[2];
+  const bool bad = fabs(lat) >= kHalfPi || fabs(y[3]) >= 100.0;
+  const double ky = bad ? kNaN : y[3], amp = y[4];
+  double g[11];
+  const auto trig = np_math::nm_sincostan_begin(lat);
+  double s, c;
+  DivGuard G;
+  KapTermsR kw;
+  const auto pending = lookup_begin(B, lon, lat, t);
+  double tn;
+  np_math::nm_sincostan_end(lat, trig, s, c, tn);
+  __builtin_amdgcn_sched_barrier(0);
+  lookup_end(B, pending, g, [&] { kw = kap_terms_r(kx, ky, G); });
+  const Merc M = merc_factors(lat, c, s);
+  double ug, vg;
+  if (RARE(!rhs_tail_fast_pair(g, M, s, c, tn, kx, kw, G, amp, B.upper, dA, dB, dC, ug, vg))) {
+    asm volatile("");   // an operand outside qdiv's exact range, or the pole band (rare branch)
+    double dy[5];
+    rhs_tail_ieee(g, M, s, c, tn, kx, ky, amp, dy, ug, vg);
+    dA = B.upper ? dy[1] : dy[0];
+    dB = B.upper ? dy[3] : dy[2];
+    dC = dy[4];
+  }
+  aux[0] = ug;
+  aux[1] = vg;
+  aux[2] = bad ? kNaN : c;
+}
+
+// the first J terms of wsum<S> for this lane's three variables (K0 = f)
+template <int S, int J>
+__device__ __forceinline__ void pair_part(const KShared<3>& K, double fA, double fB, double fC, double& pA,
+                                          double& pB, double& pC) {
+  double a = 0.0, b = 0.0, c = 0.0;
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    a = a + ((j == 0) ? fA : K.get(j, 0)) * kW[S][j];
+    b = b + ((j == 0) ? fB : K.get(j, 1)) * kW[S][j];
+    c = c + ((j == 0) ? fC : K.get(j, 2)) * kW[S][j];
+  }
+  pA = a;
+  pB = b;
+  pC = c;
+}
+__device__ __forceinline__ void pair_epart(const KShared<3>& K, double fA, double fB, double fC, double& pA,
+                                           double& pB, double& pC) {
+  double a = 0.0, b = 0.0, c = 0.0;
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    a = a + ((j == 0) ? fA : K.get(j, 0)) * kE[j];
+    b = b + ((j == 0) ? fB : K.get(j, 1)) * kE[j];
+    c = c + ((j == 0) ? fC : K.get(j, 2)) * kE[j];
+  }
+  pA = a;
+  pB = b;
+  pC = c;
+}
+
+// dp54_attempt (rkf45.py:259-321, 368-373) for a pair's ray: y, f, ynew and
+// k6 whole on both lanes; the stage values in this lane's slice of the stage
+// area (K5's, three variables of it)
+__device__ __forceinline__ double pair_attempt(const PairVaryingBG64& B, const KShared<5>& K5, double t,
+                                               const double* y, const double* f, double h, double rtol,
+                                               double atol, double* ynew, double* k6, double* aux) {
+  const bool up = B.upper;
+  KShared<3> K{K5.p, K5.stride};
+  const double yA = up ? y[1] : y[0], yB = up ? y[3] : y[2], yC = y[4];
+  const double fA = up ? f[1] : f[0], fB = up ? f[3] : f[2], fC = f[4];
+  double ys[5];
+#pragma unroll
+  for (int v = 0; v < 5; ++v) ys[v] = y[v] + wsum<1, 5>(K5, f, v) * h;   // (K unused for stage 1)
+  double ts = t + kCs[1] * h;
+  double ysA = 0.0, ysB = 0.0, ysC = 0.0, rA = 0.0, rB = 0.0, rC = 0.0, pA = 0.0, pB = 0.0, pC = 0.0;
+#pragma unroll
+  for (int s = 1; s <= 6; ++s) {
+    double w = 0.0, cn = 0.0;
+    switch (s) {
+      case 1: pair_part<2, 1>(K, fA, fB, fC, pA, pB, pC); w = kW[2][1]; cn = kCs[2]; break;
+      case 2: pair_part<3, 2>(K, fA, fB, fC, pA, pB, pC); w = kW[3][2]; cn = kCs[3]; break;
+      case 3: pair_part<4, 3>(K, fA, fB, fC, pA, pB, pC); w = kW[4][3]; cn = kCs[4]; break;
+      case 4: pair_part<5, 4>(K, fA, fB, fC, pA, pB, pC); w = kW[5][4]; cn = kCs[5]; break;
+      case 5: pair_part<6, 5>(K, fA, fB, fC, pA, pB, pC); w = kW[6][5]; cn = kCs[6]; break;
+      default: pair_epart(K, fA, fB, fC, pA, pB, pC); break;
+    }
+    pair_rhs(B, ts, ys, rA, rB, rC, aux);
+    if (s < 6) {
+      const double r3[3] = {rA, rB, rC};
+      K.put_stage(s, r3);
+      ysA = yA + (pA + rA * w) * h;
+      ysB = yB + (pB + rB * w) * h;
+      ysC = yC + (pC + rC * w) * h;
+      PairVaryingBG64::both(ysA, ys[0], ys[1]);
+      PairVaryingBG64::both(ysB, ys[2], ys[3]);
+      ys[4] = ysC;
+      ts = t + cn * h;
+    }
+  }
+  // ys = y_new, (rA, rB, rC) = K6; the error estimate of the owned variables
+#pragma unroll
+  for (int v = 0; v < 5; ++v) ynew[v] = ys[v];
+  PairVaryingBG64::both(rA, k6[0], k6[1]);
+  PairVaryingBG64::both(rB, k6[2], k6[3]);
+  k6[4] = rC;
+  const double eA = h * (pA + rA * kE[6]), eB = h * (pB + rB * kE[6]), eC = h * (pC + rC * kE[6]);
+  const double scA = atol + np_max(fabs(yA), fabs(ysA)) * rtol;
+  const double scB = atol + np_max(fabs(yB), fabs(ysB)) * rtol;
+  const double scC = atol + np_max(fabs(yC), fabs(ysC)) * rtol;
+  double xA, xB;
+  div2(eA, scA, eB, scB, xA, xB);
+  const double xC = eC / scC;
+  double x0, x1, x2, x3;
+  PairVaryingBG64::both(xA, x0, x1);
+  PairVaryingBG64::both(xB, x2, x3);
+  double ss = x0 * x0;
+  ss = ss + x1 * x1;
+  ss = ss + x2 * x2;
+  ss = ss + x3 * x3;
+  ss = ss + xC * xC;
+  return sqrt(ss) / RootN<5>::v;
+}
+template <class P>
+struct IsPair : std::false_type {};
+template <>
+struct IsPair<RayProblemT<PairVaryingBG64>> : std::true_type {};
+
 // select_initial_step (rkf45.py:34-99), direction = +1
 template <class P>
 __device__ __forceinline__ double initial_step(const P& fun, double t0, const double* y0,
@@ -2175,8 +2353,11 @@ struct Lane {
     h = tn - t;
     const double ha = fabs(h);
     double yn[NV], k6[NV];
-    double en = dp54_attempt(fun, K, t, y, f, h, rtol, atol, yn, k6, nullptr, 0,
-                             P::NAUX > 0 ? aux : nullptr);
+    double en;
+    if constexpr (IsPair<P>::value)   // (lane pairs: the split attempt)
+      en = pair_attempt(fun.B, K, t, y, f, h, rtol, atol, yn, k6, aux);
+    else
+      en = dp54_attempt(fun, K, t, y, f, h, rtol, atol, yn, k6, nullptr, 0, P::NAUX > 0 ? aux : nullptr);
     MARK("a_error_norm");
     if (en != en) en = 0.0;                 // rkf45.py:446
     // SAFETY * error_norm ** (-1/5), shared by the accept (rkf45.py:453-469) and
