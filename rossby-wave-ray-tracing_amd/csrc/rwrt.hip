@@ -1613,19 +1613,23 @@ __device__ __forceinline__ bool rhs_tail_fast(const double g[11], const Merc& M,
 // each lane divides only the numerators of its own variables by R -- the
 // lower lane dy0, dy2, the upper one dy1, dy3 (the same operation shape on
 // the other operand), both dy4 -- returned as (dA, dB, dC) (pair_attempt)
+// (The quotients that need no other quotient -- fu | fv, ux | vx over cos,
+// ug's | vg's and qk | ql -- one of each pair per lane measured no gain
+// statically: -36 VALU per attempt but +56 moves, each exchange being two
+// copies and two v_permlane32_swap per double.)
 __device__ __forceinline__ bool rhs_tail_fast_pair(const double g[11], const Merc& M, double s, double c,
                                                    double tn, double kx, const KapTermsR& kw, DivGuard G,
                                                    double amp, bool up, double& dA, double& dB, double& dC,
                                                    double& ug, double& vg) {
   const double fu = g[F_U], fv = g[F_V];
   const double rc = rcp2(c);
-  const double fmu = qdiv(fu, c, rc, G), fmv = qdiv(fv, c, rc, G);
-  const double fmux = qdiv(g[F_UX], c, rc, G), fmvx = qdiv(g[F_VX], c, rc, G);
   const double fmuy = g[F_UY] + tn * fu, fmvy = g[F_VY] + tn * fv;
   const double fmqx = g[F_QX], fmqy = g[F_QY] * c, fmqxx = g[F_QXX];
   const double fmqyx = g[F_QXY] * c, fmqxy = fmqyx;
   const double fmqyy = ((g[F_QYY] * c) - (g[F_QY] * s)) * c;
   const double kap = kw.kap, kap2 = kw.kap2;
+  const double fmu = qdiv(fu, c, rc, G), fmv = qdiv(fv, c, rc, G);
+  const double fmux = qdiv(g[F_UX], c, rc, G), fmvx = qdiv(g[F_VX], c, rc, G);
   ug = fmu + qdiv(((1.0 - kap2) * fmqy) - ((2.0 * kap) * fmqx), kw.denom, kw.rden, G);
   vg = fmv + qdiv(((2.0 * kap) * fmqy) + ((1.0 - kap2) * fmqx), kw.denom, kw.rden, G);
   const double qk = qdiv(kap * fmqxx - fmqyx, kw.kk, kw.rkk, G);
