@@ -3157,6 +3157,7 @@ __device__ __forceinline__ void run_rays(const RunArgs<BG>& a, const LBG& lbg, c
     const double tb = a.tbound[it];
     const int st = L.iterate(P, tb, a.min_step, a.rtol, a.atol, nacc, nrej);
     if (st == Lane<RayProblem, KStore>::kStep) continue;
+    MARK("x_row_end");
 
     // ---- interval it reached: post-processing (wr.py:835-885) ----
     // The last accepted step's K6 evaluation was at this y: its cos(lat), ug
@@ -3237,6 +3238,7 @@ __device__ __forceinline__ void run_rays(const RunArgs<BG>& a, const LBG& lbg, c
       ray = -1;
     }
     if ((kReplica || kPair) && it == a.it_end) ray = -1;   // (the other lanes of a latency wave or pair)
+    MARK("x_row_end_done");
   }
   if constexpr (kHandoff) {
     // Drain-time hand-off.  The queue order is a prediction (the previous
