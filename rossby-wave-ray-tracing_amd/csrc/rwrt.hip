@@ -4400,7 +4400,7 @@ using namespace rwrt;
 
 extern "C" {
 
-const char* rwrt_version(void) { return "rwrt 0.3 (gfx950, abi 3)"; }
+const char* rwrt_version(void) { return "rwrt 0.4 (gfx950, abi 4)"; }
 
 rwrt_status rwrt_ctx_create(int32_t device, rwrt_ctx** out) {
   if (!out) return fail(RWRT_ERR_ARG, "out is NULL%s");
