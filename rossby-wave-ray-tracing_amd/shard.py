@@ -34,6 +34,20 @@ import torch
 import torch.distributed as dist
 
 
+# Collectives run for groups of at least COLLECTIVE_MIN_WORLD ranks: 2 (a
+# one-rank group needs none).  A test sets 1 to drive a one-rank RCCL group
+# through the very branches an N-rank job takes -- RCCL's broadcast,
+# all_gather, gather and all_reduce on device tensors -- on a one-GPU box,
+# where RCCL refuses two ranks on one device ("Duplicate GPU detected";
+# tests/test_gpu_multirank.py::test_rccl_world1_runs_the_collective_paths).
+COLLECTIVE_MIN_WORLD = 2
+
+
+def collective(world):
+    """Whether a group of ``world`` ranks exchanges data (see COLLECTIVE_MIN_WORLD)."""
+    return world >= COLLECTIVE_MIN_WORLD
+
+
 def world_info(group=None):
     if not (dist.is_available() and dist.is_initialized()):
         return 0, 1
@@ -56,7 +70,7 @@ def shard_indices(live, rank, world):
 def broadcast_array(arr, src=0, group=None):
     """Broadcast a float64/int64 numpy array from ``src``; returns it on every rank."""
     rank, world = world_info(group)
-    if world == 1:
+    if not collective(world):
         return np.asarray(arr)
     dev = _dev(group)
     if rank == src:
@@ -86,7 +100,7 @@ def broadcast_levels(lv, make_uv, group=None, src=0, block=16):
     Returns ``{"levels", "bytes", "seconds", "collectives"}`` (bytes = what the
     broadcasts carried; 0 collectives on one rank)."""
     rank, world = world_info(group)
-    dev = _dev(group) if world > 1 else lv.device
+    dev = _dev(group) if collective(world) else lv.device
     t0 = time.perf_counter()
     nbytes = ncoll = 0
     for j0 in range(0, lv.nlev, block):
@@ -97,7 +111,7 @@ def broadcast_levels(lv, make_uv, group=None, src=0, block=16):
                 u, v = make_uv(j)
                 buf[j - j0, 0].copy_(torch.as_tensor(np.ascontiguousarray(u, np.float32)))
                 buf[j - j0, 1].copy_(torch.as_tensor(np.ascontiguousarray(v, np.float32)))
-        if world > 1:
+        if collective(world):
             dist.broadcast(buf, src, group=group)
             nbytes += buf.numel() * buf.element_size()
             ncoll += 1
@@ -111,7 +125,7 @@ def broadcast_levels(lv, make_uv, group=None, src=0, block=16):
 def reduce_summary(summary, group=None):
     """SUM of the per-rank {live rays, live rays with finite h_abs} counters."""
     rank, world = world_info(group)
-    if world == 1:
+    if not collective(world):
         return summary
     t = summary.to(_dev(group)).clone()
     dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
@@ -120,7 +134,7 @@ def reduce_summary(summary, group=None):
 
 def reduce_max(value, group=None):
     rank, world = world_info(group)
-    if world == 1:
+    if not collective(world):
         return int(value)
     t = torch.tensor([int(value)], dtype=torch.int64, device=_dev(group))
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
@@ -135,7 +149,7 @@ def gather_rows(local, idx, nray, dst=0, group=None):
     ``dst`` and ``None`` elsewhere.
     """
     rank, world = world_info(group)
-    if world == 1:
+    if not collective(world):
         out = torch.empty((nray,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
         out[torch.as_tensor(idx, device=local.device)] = local
         return out
@@ -184,7 +198,7 @@ def gather_changed_rows(local, idx, last, dst=0, group=None):
     sel = torch.nonzero(changed).squeeze(1)
     rows = bits.index_select(0, sel)
     gidx = torch.as_tensor(idx, device=local.device)[sel]
-    if world > 1:
+    if collective(world):
         dev = _dev(group)
         n = torch.tensor([int(sel.numel())], dtype=torch.int64, device=dev)
         sizes = [torch.zeros_like(n) for _ in range(world)]
@@ -262,7 +276,7 @@ def probe_costs(eng, st, p, tb, npr, rank, world, group=None):
         out = torch.full((m,), -2, dtype=torch.int64, device=dev)
         out[: v.numel()] = v
         return out
-    if group is not None and world > 1:
+    if group is not None and collective(world):
         mine = one(rank)
         cdev = _dev(group)
         parts = [torch.empty(m, dtype=torch.int64, device=cdev) for _ in range(world)]
@@ -328,7 +342,7 @@ def run_sharded(eng, y0, nt, tstep=7200.0, group=None, rank=None, world=None, pr
     npr = min(probe, nt - 1)
     if events is not None:
         e0, e1, es = eng._event_pair()
-    if world > 1 and (shard_probe or costs is not None):
+    if collective(world) and (shard_probe or costs is not None):
         if costs is None:
             cost, frozen = probe_costs(eng, st, p, tb, npr, rank, world, group=group)
         else:   # (a rehearsal: the other shares were probed beforehand)
@@ -396,7 +410,7 @@ def run_sharded(eng, y0, nt, tstep=7200.0, group=None, rank=None, world=None, pr
     ends = cnts = None
     if gather:
         end_row = last["row"].clone()
-        if group is not None and world > 1:
+        if group is not None and collective(world):
             ends = gather_rows(end_row, idx.cpu().numpy(), nray, group=group)
             cnts = gather_rows(local["count"], idx.cpu().numpy(), nray, group=group)
         else:   # (one rank, or one emulated rank of a larger job: its own rays, in idx order)

@@ -163,7 +163,8 @@ class WR:
         import torch
         import shard
         rank, world = shard.world_info(group) if group is not None else (0, 1)
-        if world > 1:
+        multi = group is not None and shard.collective(world)
+        if multi:
             self.bs.fields = shard.broadcast_array(self.bs.fields, 0, group)
             self.bs._engine = None
         eng = self.bs.engine()
@@ -171,12 +172,12 @@ class WR:
         y0 = np.array([self.rlon[0], self.rlat[0], self.rzwn[0], self.rmwn[0],
                        self.ramp[0]], dtype=self.all_dtype).reshape(5, nray)
         idx = np.arange(nray)
-        if world > 1:
+        if multi:
             idx = shard.shard_indices(~np.isnan(y0.mean(axis=0)), rank, world)
         rows_shape = (3, self.nsource, self.nzwn)
         hist = (self.rlon, self.rlat, self.rzwn, self.rmwn, self.ramp, self.rug, self.rvg)
 
-        if world > 1:
+        if multi:
             # each rank's previous rows (row 0: the initial rows), as bit patterns
             row0 = np.stack([h[0].reshape(-1)[idx] for h in hist], axis=1)
             last = torch.as_tensor(np.ascontiguousarray(row0)).view(torch.int64).to(eng.device)
@@ -198,9 +199,9 @@ class WR:
                 progress_bar(i1 - 1, self.nt)
 
         chunk = self.chunk_rows or _default_chunk(nray, self.nt)
-        grp = group if world > 1 else None
+        grp = group if multi else None
         out, hs = None, None
-        if world == 1:
+        if not multi:
             # single GPU: chunks reach the host arrays while the next one is
             # computed (permute on the device, pinned D2H, threaded copies)
             from hostio import HistorySink

@@ -31,11 +31,18 @@ def fake_integrate(y0):
     return torch.stack([rows, rows * 2, rows * 3], 1)
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, min_world=2):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    ncoll = []
+    for name in ("broadcast", "all_reduce", "all_gather", "gather"):
+        def counted(*a, _f=getattr(dist, name), **k):
+            ncoll.append(1)
+            return _f(*a, **k)
+        setattr(dist, name, counted)
     try:
         import shard
+        shard.COLLECTIVE_MIN_WORLD = min_world
         rng = np.random.default_rng(0)
         nray = 101
         y0 = rng.standard_normal((5, nray)) if rank == 0 else None
@@ -49,7 +56,7 @@ def _worker(rank, world, port, q):
         mx = shard.reduce_max(10 + rank)
         if rank == 0:
             q.put(("ok", full.numpy(), fake_integrate(y0).numpy(), summ.tolist(), mx,
-                   int(live.sum())))
+                   int(live.sum()), len(ncoll)))
     except Exception as e:  # pragma: no cover
         q.put(("err", repr(e)))
         raise
@@ -78,10 +85,30 @@ def test_world2_gloo_pipeline_equals_unsharded():
     for p in procs:
         p.join(timeout=60)
     assert res[0] == "ok", res
-    _, full, ref, summ, mx, nlive = res
+    _, full, ref, summ, mx, nlive, ncoll = res
     assert np.array_equal(full, ref, equal_nan=True)
     assert summ == [nlive, 1]
     assert mx == 11
+    assert ncoll >= 7
+
+
+@pytest.mark.parametrize("min_world,ncoll", [(2, 0), (1, 7)])
+def test_world1_collective_knob(min_world, ncoll):
+    """One rank: no collective by default; with shard.COLLECTIVE_MIN_WORLD = 1
+    the N-rank branches run (2 broadcasts, all_gather + 2 gathers, 2
+    all_reduces) and give the same result (tests/test_gpu_multirank.py drives
+    RCCL this way on the one-GPU box)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_worker, args=(0, 1, _free_port(), q, min_world))
+    p.start()
+    res = q.get(timeout=120)
+    p.join(timeout=60)
+    assert res[0] == "ok", res
+    _, full, ref, summ, mx, nlive, n = res
+    assert np.array_equal(full, ref, equal_nan=True)
+    assert summ == [nlive, 0] and mx == 10
+    assert n == ncoll
 
 
 @pytest.mark.parametrize("world", [1, 2, 4, 8])
